@@ -1,0 +1,213 @@
+"""Benchmark of the volumetric triangulation hot path on MI355X.
+
+Metric (BASELINE.json): multiview frames/sec (4-view x 64^3 unproject + soft-argmax).
+One "step" = one pass of the hot path over one batch of synthetic frames resident in
+HBM:  unproject_heatmaps(softmax aggregation) -> integrate_tensor_3d_with_coordinates
+over channels [0:17] of the unprojected volume (the stand-in for V2V)
+-> (N > 1) one all-gather of the (B/N, 17, 3) joints over RCCL.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--no-cpu-baseline]
+
+N > 1 is launched by torch.distributed.run (one process per GPU); every rank builds its
+own frames from (seed, global frame index) — weak scaling, fixed frames per GPU.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "learnable-triangulation-pytorch_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from mvn_rocm import op, synth  # noqa: E402
+
+METRIC = "multiview frames/sec (4-view x 64^3 unproject+soft-argmax), 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# BASELINE.json configs (per GPU): name -> (views, channels, heatmap, volume, joints, frames/GPU, dtype)
+CONFIGS = {
+    "2": dict(views=4, channels=32, heatmap=96, volume=64, joints=17, frames=8, dtype=torch.float32,
+              label="cfg2: 4 views x 32 ch x 96^2 -> 64^3 unproject(softmax agg) + 17-joint soft-argmax, fp32"),
+    "3": dict(views=4, channels=32, heatmap=96, volume=64, joints=17, frames=32, dtype=torch.bfloat16,
+              label="cfg3: 4 views x 32 ch x 96^2 -> 64^3 unproject(softmax agg) + 17-joint soft-argmax, bf16"),
+    "4": dict(views=8, channels=32, heatmap=96, volume=64, joints=17, frames=16, dtype=torch.float32,
+              label="cfg4: 8 views (CMU-style) x 32 ch x 96^2 -> 64^3 unproject + soft-argmax, fp32"),
+}
+
+
+def unproject_bytes(c, E):
+    """Algorithmic bytes of one frame's unprojection: features read once,
+    volume written once, coordinates read once (f32), projections read."""
+    V3 = c["volume"] ** 3
+    return E * (c["views"] * c["channels"] * c["heatmap"] ** 2 + c["channels"] * V3) + 4 * 3 * V3 + 4 * 12 * c["views"]
+
+
+def frame_bytes(c, E):
+    """Whole-path algorithmic bytes per frame (SURVEY.md §8d / BASELINE.md §4)."""
+    V3 = c["volume"] ** 3
+    return (E * (c["views"] * c["channels"] * c["heatmap"] ** 2 + c["channels"] * V3 + 2 * c["joints"] * V3)
+            + 4 * (2 * 3 * V3) + 4 * (12 * c["views"] + 3 * c["joints"]))
+
+
+def dtype_name(dt):
+    return {torch.float32: "f32", torch.bfloat16: "bf16"}[dt]
+
+
+class Workload:
+    def __init__(self, cfg, rank, world, device, seed=0):
+        self.cfg, self.rank, self.world, self.device = cfg, rank, world, device
+        B = cfg["frames"]
+        vb = synth.volumetric_batch(B, n_views=cfg["views"], channels=cfg["channels"], heatmap=cfg["heatmap"],
+                                    volume=cfg["volume"], dtype=cfg["dtype"], device=device, seed=seed,
+                                    first_frame=rank * B)
+        self.feat, self.proj, self.coords = vb.features, vb.proj, vb.coords
+        self.gathered = torch.empty((world * B, cfg["joints"], 3), device=device) if world > 1 else None
+        self.ev = []
+
+    def step(self, timed=False):
+        J = self.cfg["joints"]
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        vol = op.unproject_heatmaps(self.feat, self.proj, self.coords, "softmax")
+        if timed:
+            e1.record()
+            self.ev.append((e0, e1))
+        xyz, sm = op.integrate_tensor_3d_with_coordinates(vol[:, :J], self.coords, True)
+        if self.gathered is not None:
+            dist.all_gather_into_tensor(self.gathered, xyz)
+        return xyz, sm
+
+    def unproject_ms(self):
+        torch.cuda.synchronize()
+        t = [a.elapsed_time(b) for a, b in self.ev]
+        return sum(t) / len(t)
+
+
+def run_config(name, args, rank, world, device):
+    cfg = CONFIGS[name]
+    wl = Workload(cfg, rank, world, device)
+    for _ in range(args.warmup):
+        wl.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step(timed=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    E = 2 if cfg["dtype"] == torch.bfloat16 else 4
+    frames_total = cfg["frames"] * world * args.steps
+    unproj_ms = wl.unproject_ms()
+    launch_bytes = unproject_bytes(cfg, E) * cfg["frames"]
+    achieved = launch_bytes / (unproj_ms * 1e-3) / 1e9
+    return dict(
+        cfg=cfg, elapsed=elapsed, fps=frames_total / elapsed, ms_per_step=elapsed / args.steps * 1e3,
+        unproject_ms=unproj_ms, launch_bytes=launch_bytes, achieved_gbps=achieved,
+        path_gbps=frame_bytes(cfg, E) * frames_total / elapsed / 1e9)
+
+
+def cpu_baseline(seconds=15.0):
+    """The reference algorithm restated op-for-op in torch-CPU (oracle/restate_torch.py),
+    timed on this host on one frame of config 2 at a time (bounded sample)."""
+    from oracle import restate_torch
+    import warnings
+    warnings.filterwarnings("ignore")
+    vb = synth.volumetric_batch(1, seed=0)
+    cfg = CONFIGS["2"]
+    n, t0 = 0, time.perf_counter()
+    while True:
+        vol = restate_torch.unproject_heatmaps(vb.features, vb.proj, vb.coords, "softmax")
+        restate_torch.integrate_tensor_3d_with_coordinates(vol[:, :cfg["joints"]], vb.coords, True)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 50:
+            break
+    return dict(value=n / el, unit="frames/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"{n} frame(s) of config 2 (4x32x96^2 -> 64^3, softmax agg, 17-joint soft-argmax, fp32) "
+                       f"through oracle/restate_torch.py in {el:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    main_res = run_config(args.config, args, rank, world, device)
+    secondary = None
+    if not args.no_secondary and args.config == "2":
+        s = run_config("3", args, rank, world, device)
+        secondary = dict(workload=s["cfg"]["label"], value=s["fps"], unit="frames/s", ms_per_step=s["ms_per_step"],
+                         frames_per_gpu=s["cfg"]["frames"], unproject_ms=s["unproject_ms"],
+                         unproject_achieved_gbps=s["achieved_gbps"],
+                         unproject_frac=s["achieved_gbps"] / HBM_PEAK_GBPS,
+                         path_algorithmic_gbps=s["path_gbps"], path_frac=s["path_gbps"] / HBM_PEAK_GBPS)
+    base = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        base = cpu_baseline()
+
+    if rank == 0:
+        r, c = main_res, main_res["cfg"]
+        line = {
+            "metric": METRIC,
+            "value": r["fps"],
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": r["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": dtype_name(c["dtype"]),
+            "data": "synthetic (seeded ring cameras, N(0,1) features, rotated 2.5 m cuboids; SURVEY.md §8d)",
+            "config": {"workload": c["label"], "global_batch": c["frames"] * world, "frames_per_gpu": c["frames"],
+                       "views": c["views"], "channels": c["channels"], "heatmap": c["heatmap"],
+                       "volume": c["volume"], "joints": c["joints"], "parallelism": f"dp{world}",
+                       "collective": "all_gather joints (RCCL)" if world > 1 else None},
+            "roofline": {"kernel": "unproject_regviews<softmax>", "bound": "hbm",
+                         "achieved": r["achieved_gbps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": r["achieved_gbps"] / HBM_PEAK_GBPS, "traffic": None,
+                         "launch_ms": r["unproject_ms"], "algorithmic_bytes_per_launch": r["launch_bytes"]},
+            "path_algorithmic_gbps": r["path_gbps"],
+            "cpu_baseline": base,
+            "secondary": secondary,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

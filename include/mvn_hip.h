@@ -1,0 +1,123 @@
+/*
+ * mvn_hip.h — C ABI of libmvn_hip.so, the MI355X (gfx950) implementation of the
+ * volumetric / algebraic triangulation hot path of learnable-triangulation-pytorch.
+ *
+ * The reference has no FFI layer: its boundary is three module-level Python
+ * functions that the models call by attribute lookup.  Each entry
+ * point below replaces exactly one of them and is what a ctypes / torch custom-op
+ * binding on the reference side would call:
+ *
+ *   mvn_unproject        <- mvn/utils/op.py:99-163   unproject_heatmaps(...)
+ *   mvn_softargmax3d     <- mvn/utils/op.py:84-96    integrate_tensor_3d_with_coordinates(...)
+ *   mvn_dlt              <- mvn/utils/multiview.py:162-174 triangulate_batch_of_points(...)
+ *                           (+ its per-point solver multiview.py:132-159)
+ *
+ * Conventions
+ *   - Every buffer is caller-owned device memory (hipMalloc / torch), contiguous,
+ *     row-major in the reference's own tensor layout.  Nothing is retained after
+ *     return; nothing is allocated (soft-argmax takes a caller workspace).
+ *   - `stream` is a hipStream_t passed as void* (0 = the null stream).  Every call
+ *     is stream-ordered and asynchronous: no host synchronisation, capturable in a
+ *     hipGraph.
+ *   - Return value: MVN_OK (0) or a negative MVN_ERR_* code.  Argument checks run
+ *     before any HIP call, so they are safe without a GPU.
+ *   - Functions are reentrant; the library keeps no mutable global state.
+ */
+#ifndef MVN_HIP_H
+#define MVN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ------------------------------------------------------- */
+#define MVN_OK              0
+#define MVN_ERR_ARG        -1   /* null pointer / bad enum / bad flag            */
+#define MVN_ERR_SHAPE      -2   /* non-positive or overflowing extent            */
+#define MVN_ERR_DTYPE      -3   /* unsupported dtype combination                 */
+#define MVN_ERR_LAUNCH     -4   /* hipLaunchKernel / hipGetLastError failed      */
+#define MVN_ERR_WORKSPACE  -5   /* workspace missing or too small                */
+
+/* ---- dtypes ------------------------------------------------------------ */
+#define MVN_DTYPE_F32   0
+#define MVN_DTYPE_BF16  1
+
+/* ---- view aggregation (op.py:147-161) ---------------------------------- */
+#define MVN_AGG_SUM      0     /* 'sum'                                           */
+#define MVN_AGG_MAX      1     /* 'max'                                           */
+#define MVN_AGG_SOFTMAX  2     /* 'softmax'                                       */
+#define MVN_AGG_CONF     3     /* any string starting with 'conf' (op.py:147)     */
+
+/* Library version, (major << 16) | (minor << 8) | patch. */
+int mvn_version(void);
+
+/* Static message for an MVN_* return code. */
+const char* mvn_strerror(int code);
+
+/*
+ * Unprojection of N views of C-channel maps into a C x Vx x Vy x Vz volume.
+ * Replaces mvn/utils/op.py:99-163 (unproject_heatmaps).
+ *
+ *   feat    (B, N, C, H, W)     feat_dtype (f32 | bf16)
+ *   proj    (B, N, 3, 4)        f32, heatmap-resolution projection matrices
+ *   coords  (B, Vx, Vy, Vz, 3)  f32 world coordinates per voxel
+ *   conf    (B, N, C)           f32, read only when agg == MVN_AGG_CONF (else may be NULL)
+ *   out     (B, C, Vx, Vy, Vz)  out_dtype (f32 | bf16)
+ *   align_corners: 0 = torch>=1.3 grid_sample default (the importable oracle),
+ *                  1 = torch 1.0.1 semantics (requirements.txt:20 pins 1.0.1).
+ */
+int mvn_unproject(const void* feat, int feat_dtype,
+                  const float* proj, const float* coords, const float* conf,
+                  void* out, int out_dtype,
+                  int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+                  int agg, int align_corners, void* stream);
+
+/*
+ * 3D soft-argmax over voxel world coordinates.
+ * Replaces mvn/utils/op.py:84-96 (integrate_tensor_3d_with_coordinates), with the
+ * caller's `volumes * volume_multiplier` (triangulation.py:353) fused as `multiplier`.
+ *
+ *   vol       element (b, j, i) at vol[b*vol_bstride + j*vol_jstride + i], i < Vx*Vy*Vz
+ *             (strides in elements, so a channel slice of an unprojected volume
+ *             needs no copy); vol_dtype f32 | bf16
+ *   coords    (B, Vx, Vy, Vz, 3) f32
+ *   out_xyz   (B, J, 3) f32
+ *   out_vol   (B, J, Vx, Vy, Vz) contiguous, out_dtype f32 | bf16; NULL = do not
+ *             write the normalised volume
+ *   softmax   1 = softmax over the flattened volume (op.py:89),
+ *             0 = relu with no mass normalisation (op.py:91, reference quirk)
+ *   workspace >= mvn_softargmax3d_workspace_bytes(B, J, Vx, Vy, Vz) bytes of
+ *             device memory, 16-byte aligned; contents need no initialisation.
+ */
+size_t mvn_softargmax3d_workspace_bytes(int B, int J, int Vx, int Vy, int Vz);
+
+int mvn_softargmax3d(const void* vol, int vol_dtype,
+                     int64_t vol_bstride, int64_t vol_jstride,
+                     const float* coords, float multiplier, int softmax,
+                     float* out_xyz, void* out_vol, int out_dtype,
+                     void* workspace, size_t workspace_bytes,
+                     int B, int J, int Vx, int Vy, int Vz, void* stream);
+
+/*
+ * Confidence-weighted linear (DLT) triangulation of a batch of points.
+ * Replaces mvn/utils/multiview.py:162-174 (triangulate_batch_of_points) and its
+ * per-point solver multiview.py:132-159.  The 2N x 4 design matrix is formed in
+ * f32 exactly as the reference forms it (multiview.py:150-152); its null vector is
+ * found in f64 (streaming Givens QR + one-sided Jacobi SVD).
+ *
+ *   proj  (B, N, 3, 4) f32     image-resolution projection matrices
+ *   pts   (B, N, J, 2) f32     2D points, pixels
+ *   conf  (B, N, J)    f32     per-view confidences; NULL = all ones (multiview.py:147-148)
+ *   out   (B, J, 3)    f32
+ */
+int mvn_dlt(const float* proj, const float* pts, const float* conf, float* out,
+            int B, int N, int J, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MVN_HIP_H */

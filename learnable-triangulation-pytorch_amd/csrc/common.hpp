@@ -1,0 +1,44 @@
+// Shared device helpers for libmvn_hip (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mvn_hip.h"
+
+namespace mvn {
+
+constexpr int kWave = 64;
+
+// ---- element access ------------------------------------------------------
+// bf16 is carried as raw uint16_t bits; widening is exact (bits << 16).
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(uint16_t v) { return __uint_as_float(uint32_t(v) << 16); }
+
+// Round-to-nearest-even f32 -> bf16 with NaN kept a NaN.
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return uint16_t((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return uint16_t(u >> 16);
+}
+
+template <typename T> __device__ __forceinline__ void store_elem(T* p, float v);
+template <> __device__ __forceinline__ void store_elem<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void store_elem<uint16_t>(uint16_t* p, float v) { *p = f32_to_bf16(v); }
+
+// ---- wave reductions (64 lanes) -----------------------------------------
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
+
+}  // namespace mvn

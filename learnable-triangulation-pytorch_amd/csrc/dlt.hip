@@ -1,0 +1,157 @@
+// Batched confidence-weighted algebraic (DLT) triangulation for gfx950.
+//
+// Replaces mvn/utils/multiview.py:162-174 (triangulate_batch_of_points) and its
+// per-point solver multiview.py:132-159.  The reference loops over B x J in Python
+// and calls torch.svd on each 2N x 4 matrix (B*J LAPACK / rocSOLVER calls).
+//
+// Here one lane owns one (b, j):
+//   1. rows of A are formed in f32 exactly as multiview.py:150-152 forms them
+//      (A = P[2]*pt; A -= P[:2]; A *= conf — three separately rounded ops),
+//   2. each row is folded into a 4x4 upper-triangular R by Givens rotations (f64),
+//      so R^T R = A^T A without ever squaring the condition number and for any N,
+//   3. a one-sided Jacobi SVD of R (f64) gives the right singular vectors; the one
+//      of the smallest singular value is the homogeneous point (multiview.py:154-156),
+//   4. X[:3] / X[3] (multiview.py:157; sign of the null vector cancels).
+#include "common.hpp"
+
+namespace mvn {
+namespace {
+
+constexpr int kDltBlock = 64;
+
+__device__ __forceinline__ void givens_fold(double (&R)[4][4], double (&a)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (a[k] == 0.0) continue;
+    const double r = hypot(R[k][k], a[k]);
+    const double c = R[k][k] / r, s = a[k] / r;
+    R[k][k] = r;
+    a[k] = 0.0;
+#pragma unroll
+    for (int l = k + 1; l < 4; ++l) {
+      const double rk = R[k][l], al = a[l];
+      R[k][l] = c * rk + s * al;
+      a[l] = -s * rk + c * al;
+    }
+  }
+}
+
+// One-sided Jacobi on the columns of U (= R on entry); V accumulates the rotations.
+__device__ __forceinline__ void jacobi_svd(double (&U)[4][4], double (&V)[4][4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) V[i][k] = i == k ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    bool rotated = false;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int q = p + 1; q < 4; ++q) {
+        double alpha = 0.0, beta = 0.0, gamma = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          alpha += U[i][p] * U[i][p];
+          beta += U[i][q] * U[i][q];
+          gamma += U[i][p] * U[i][q];
+        }
+        if (gamma == 0.0 || fabs(gamma) <= 1e-15 * sqrt(alpha * beta)) continue;
+        rotated = true;
+        const double zeta = (beta - alpha) / (2.0 * gamma);
+        const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const double up = U[i][p], uq = U[i][q];
+          U[i][p] = c * up - s * uq;
+          U[i][q] = s * up + c * uq;
+          const double vp = V[i][p], vq = V[i][q];
+          V[i][p] = c * vp - s * vq;
+          V[i][q] = s * vp + c * vq;
+        }
+      }
+    if (!rotated) break;
+  }
+}
+
+__global__ __launch_bounds__(kDltBlock) void dlt_kernel(const float* __restrict__ P, const float* __restrict__ pts,
+                                                        const float* __restrict__ conf, float* __restrict__ out,
+                                                        int B, int N, int J) {
+  const int t = blockIdx.x * kDltBlock + threadIdx.x;
+  if (t >= B * J) return;
+  const int b = t / J, j = t - b * J;
+
+  double R[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) R[i][k] = 0.0;
+
+  for (int v = 0; v < N; ++v) {
+    const float* Pv = P + (size_t(b) * N + v) * 12;
+    const size_t pj = (size_t(b) * N + v) * J + j;
+    const float pt[2] = {pts[pj * 2 + 0], pts[pj * 2 + 1]};
+    const float cf = conf ? conf[pj] : 1.f;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      double a[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float e = Pv[8 + k] * pt[r];   // multiview.py:150
+        e = e - Pv[r * 4 + k];         // multiview.py:151
+        e = e * cf;                    // multiview.py:152
+        a[k] = double(e);
+      }
+      givens_fold(R, a);
+    }
+  }
+
+  double V[4][4];
+  jacobi_svd(R, V);
+  int kmin = 0;
+  double smin = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double n2 = R[0][k] * R[0][k] + R[1][k] * R[1][k] + R[2][k] * R[2][k] + R[3][k] * R[3][k];
+    if (k == 0 || n2 < smin) { smin = n2; kmin = k; }
+  }
+  double X[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    X[i] = V[i][0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) if (kmin == k) X[i] = V[i][k];
+  }
+  float* o = out + size_t(t) * 3;
+  o[0] = float(X[0] / X[3]);
+  o[1] = float(X[1] / X[3]);
+  o[2] = float(X[2] / X[3]);
+}
+
+}  // namespace
+}  // namespace mvn
+
+extern "C" int mvn_dlt(const float* proj, const float* pts, const float* conf, float* out, int B, int N, int J,
+                       void* stream) {
+  using namespace mvn;
+  if (!proj || !pts || !out) return MVN_ERR_ARG;
+  if (B <= 0 || N <= 0 || J <= 0) return MVN_ERR_SHAPE;
+  if ((long long)B * J > (1LL << 30)) return MVN_ERR_SHAPE;
+  const int n = B * J;
+  dlt_kernel<<<(n + kDltBlock - 1) / kDltBlock, kDltBlock, 0, static_cast<hipStream_t>(stream)>>>(proj, pts, conf, out, B, N, J);
+  return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
+}
+
+extern "C" int mvn_version(void) { return (0 << 16) | (1 << 8) | 0; }
+
+extern "C" const char* mvn_strerror(int code) {
+  switch (code) {
+    case MVN_OK: return "ok";
+    case MVN_ERR_ARG: return "invalid argument (null pointer, enum or flag)";
+    case MVN_ERR_SHAPE: return "invalid shape (non-positive or too large extent)";
+    case MVN_ERR_DTYPE: return "unsupported dtype combination";
+    case MVN_ERR_LAUNCH: return "HIP kernel launch failed";
+    case MVN_ERR_WORKSPACE: return "workspace missing or too small";
+  }
+  return "unknown error";
+}

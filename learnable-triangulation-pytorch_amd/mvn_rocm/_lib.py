@@ -1,0 +1,64 @@
+"""ctypes binding of libmvn_hip.so (the C ABI declared in include/mvn_hip.h).
+
+The shared library is built in-tree (``make -C learnable-triangulation-pytorch_amd``)
+and loaded from this directory.  There is no CPU fallback anywhere in the product
+path: if the library is missing, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmvn_hip.so")
+
+MVN_OK = 0
+MVN_DTYPE_F32 = 0
+MVN_DTYPE_BF16 = 1
+MVN_AGG_SUM, MVN_AGG_MAX, MVN_AGG_SOFTMAX, MVN_AGG_CONF = 0, 1, 2, 3
+
+_c_int, _c_void_p, _c_float, _c_i64, _c_size_t = (
+    ctypes.c_int, ctypes.c_void_p, ctypes.c_float, ctypes.c_int64, ctypes.c_size_t)
+
+# name -> (restype, argtypes); kept in the order of include/mvn_hip.h
+SIGNATURES = {
+    "mvn_version": (_c_int, []),
+    "mvn_strerror": (ctypes.c_char_p, [_c_int]),
+    "mvn_unproject": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int]
+                      + [_c_int] * 8 + [_c_int, _c_int, _c_void_p]),
+    "mvn_softargmax3d_workspace_bytes": (_c_size_t, [_c_int] * 5),
+    "mvn_softargmax3d": (_c_int, [_c_void_p, _c_int, _c_i64, _c_i64, _c_void_p, _c_float, _c_int,
+                                  _c_void_p, _c_void_p, _c_int, _c_void_p, _c_size_t]
+                         + [_c_int] * 5 + [_c_void_p]),
+    "mvn_dlt": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_void_p]),
+}
+
+_lib = None
+
+
+class MvnError(RuntimeError):
+    """A negative MVN_ERR_* code returned by libmvn_hip."""
+
+
+def load():
+    """Load (once) and return the ctypes handle; raise loudly if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libmvn_hip.so not found at {LIB_PATH}; build it with "
+                "`make -C learnable-triangulation-pytorch_amd` (or __graft_entry__.build()). "
+                "mvn_rocm has no CPU fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(code: int, what: str) -> None:
+    if code != MVN_OK:
+        msg = load().mvn_strerror(code).decode()
+        raise MvnError(f"{what}: {msg} (code {code})")

@@ -1,0 +1,116 @@
+"""PyTorch-ROCm custom ops over the libmvn_hip C ABI.
+
+Each op is registered with ``torch.library.custom_op`` under the ``mvn_rocm``
+namespace (``torch.ops.mvn_rocm.unproject`` …), launches on torch's current HIP
+stream of the input's device, and has a fake (meta) kernel so it traces.  Inputs
+must already live on the GPU: there is deliberately no CPU path.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+
+_DTYPE_CODE = {torch.float32: _lib.MVN_DTYPE_F32, torch.bfloat16: _lib.MVN_DTYPE_BF16}
+_CODE_DTYPE = {v: k for k, v in _DTYPE_CODE.items()}
+
+
+def _stream(t: Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _require_gpu(*tensors: Optional[Tensor]) -> None:
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                "mvn_rocm ops run on the MI355X only (got a tensor on "
+                f"{t.device}); there is no CPU fallback")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"mvn_rocm: tensors on different devices ({dev} vs {t.device})")
+
+
+def _ptr(t: Optional[Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+# --------------------------------------------------------------------------- unproject
+@torch.library.custom_op("mvn_rocm::unproject", mutates_args=())
+def unproject(feat: Tensor, proj: Tensor, coords: Tensor, conf: Optional[Tensor], agg: int,
+              align_corners: bool, out_dtype: int) -> Tensor:
+    """feat (B,N,C,H,W) f32|bf16, proj (B,N,3,4) f32, coords (B,Vx,Vy,Vz,3) f32,
+    conf (B,N,C) f32 or None -> (B,C,Vx,Vy,Vz) of dtype code `out_dtype`."""
+    _require_gpu(feat, proj, coords, conf)
+    B, N, C, H, W = feat.shape
+    Vx, Vy, Vz = coords.shape[1:4]
+    out = torch.empty((B, C, Vx, Vy, Vz), dtype=_CODE_DTYPE[out_dtype], device=feat.device)
+    code = _lib.load().mvn_unproject(
+        feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), coords.data_ptr(), _ptr(conf),
+        out.data_ptr(), out_dtype, B, N, C, H, W, Vx, Vy, Vz, agg, int(align_corners), _stream(feat))
+    _lib.check(code, "mvn_unproject")
+    return out
+
+
+@unproject.register_fake
+def _(feat, proj, coords, conf, agg, align_corners, out_dtype):
+    B, N, C, H, W = feat.shape
+    return feat.new_empty((B, C, *coords.shape[1:4]), dtype=_CODE_DTYPE[out_dtype])
+
+
+# --------------------------------------------------------------------------- soft-argmax
+@torch.library.custom_op("mvn_rocm::softargmax3d", mutates_args=())
+def softargmax3d(vol: Tensor, coords: Tensor, softmax: bool, multiplier: float, return_volume: bool,
+                 out_dtype: int) -> Tuple[Tensor, Tensor]:
+    """vol (B,J,Vx,Vy,Vz) f32|bf16 (inner three dims contiguous; batch / joint strides
+    arbitrary), coords (B,Vx,Vy,Vz,3) f32 -> (xyz (B,J,3) f32, normalised volume or an
+    empty tensor when return_volume is False)."""
+    _require_gpu(vol, coords)
+    B, J, Vx, Vy, Vz = vol.shape
+    xyz = torch.empty((B, J, 3), dtype=torch.float32, device=vol.device)
+    if return_volume:
+        out = torch.empty((B, J, Vx, Vy, Vz), dtype=_CODE_DTYPE[out_dtype], device=vol.device)
+    else:
+        out = torch.empty((0,), dtype=_CODE_DTYPE[out_dtype], device=vol.device)
+    lib = _lib.load()
+    ws_bytes = lib.mvn_softargmax3d_workspace_bytes(B, J, Vx, Vy, Vz)
+    ws = torch.empty((ws_bytes + 15) // 16 * 4, dtype=torch.float32, device=vol.device)
+    code = lib.mvn_softargmax3d(
+        vol.data_ptr(), _DTYPE_CODE[vol.dtype], vol.stride(0), vol.stride(1), coords.data_ptr(),
+        float(multiplier), int(softmax), xyz.data_ptr(), out.data_ptr() if return_volume else None,
+        out_dtype, ws.data_ptr(), ws.numel() * 4, B, J, Vx, Vy, Vz, _stream(vol))
+    _lib.check(code, "mvn_softargmax3d")
+    return xyz, out
+
+
+@softargmax3d.register_fake
+def _(vol, coords, softmax, multiplier, return_volume, out_dtype):
+    B, J = vol.shape[:2]
+    xyz = vol.new_empty((B, J, 3), dtype=torch.float32)
+    shape = tuple(vol.shape) if return_volume else (0,)
+    return xyz, vol.new_empty(shape, dtype=_CODE_DTYPE[out_dtype])
+
+
+# --------------------------------------------------------------------------- DLT
+@torch.library.custom_op("mvn_rocm::dlt", mutates_args=())
+def dlt(proj: Tensor, pts: Tensor, conf: Optional[Tensor]) -> Tensor:
+    """proj (B,N,3,4) f32, pts (B,N,J,2) f32, conf (B,N,J) f32 or None -> (B,J,3) f32."""
+    _require_gpu(proj, pts, conf)
+    B, N, J = pts.shape[:3]
+    out = torch.empty((B, J, 3), dtype=torch.float32, device=pts.device)
+    code = _lib.load().mvn_dlt(proj.data_ptr(), pts.data_ptr(), _ptr(conf), out.data_ptr(), B, N, J,
+                               _stream(pts))
+    _lib.check(code, "mvn_dlt")
+    return out
+
+
+@dlt.register_fake
+def _(proj, pts, conf):
+    B, N, J = pts.shape[:3]
+    return pts.new_empty((B, J, 3), dtype=torch.float32)

@@ -1,0 +1,117 @@
+"""Drop-in replacements for the hot-path functions of ``mvn/utils/op.py``.
+
+Same names, positional / keyword order, defaults, return values and exception
+types as the reference (cited per function).  Extra keyword-only arguments have
+defaults that reproduce the reference behaviour.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from . import _ops
+
+_AGG = {"sum": _lib.MVN_AGG_SUM, "max": _lib.MVN_AGG_MAX, "softmax": _lib.MVN_AGG_SOFTMAX}
+
+
+def aggregation_code(method: str) -> int:
+    """Map the reference's aggregation string to its code (op.py:147-161)."""
+    if method.startswith("conf"):          # op.py:147 — any 'conf*' string
+        return _lib.MVN_AGG_CONF
+    if method in _AGG:
+        return _AGG[method]
+    raise ValueError("Unknown volume_aggregation_method: {}".format(method))   # op.py:161
+
+
+def _dtype_code(dtype: torch.dtype) -> int:
+    if dtype == torch.float32:
+        return _lib.MVN_DTYPE_F32
+    if dtype == torch.bfloat16:
+        return _lib.MVN_DTYPE_BF16
+    raise TypeError(f"mvn_rocm supports float32 and bfloat16, got {dtype}")
+
+
+def unproject_heatmaps(heatmaps, proj_matricies, coord_volumes, volume_aggregation_method='sum',
+                       vol_confidences=None, *, align_corners=False, out_dtype=None):
+    """Lift N views of C-channel maps into a (B, C, Vx, Vy, Vz) volume.
+
+    Reference: ``mvn/utils/op.py:99-163``.
+      heatmaps (B, N, C, H, W), proj_matricies (B, N, 3, 4), coord_volumes (B, Vx, Vy, Vz, 3),
+      volume_aggregation_method in {'sum', 'max', 'softmax', 'conf*'}, vol_confidences (B, N, C).
+    ``align_corners`` selects grid_sample semantics (False = torch>=1.3, the importable
+    oracle; True = the torch 1.0.1 the reference pins).  ``out_dtype`` defaults to the
+    heatmap dtype (float32 for float32 input, as in the reference).
+    """
+    agg = aggregation_code(volume_aggregation_method)
+    if agg == _lib.MVN_AGG_CONF and vol_confidences is None:
+        raise TypeError("volume_aggregation_method '{}' needs vol_confidences".format(volume_aggregation_method))
+    feat = heatmaps.contiguous()
+    if feat.dtype not in (torch.float32, torch.bfloat16):
+        feat = feat.float()
+    proj = proj_matricies.float().contiguous()
+    coords = coord_volumes.float().contiguous()
+    conf = vol_confidences.float().contiguous() if agg == _lib.MVN_AGG_CONF else None
+    if proj.shape[:2] != feat.shape[:2] or proj.shape[2:] != (3, 4):
+        raise RuntimeError(f"proj_matricies shape {tuple(proj.shape)} does not match heatmaps {tuple(feat.shape)}")
+    if coords.dim() != 5 or coords.shape[0] != feat.shape[0] or coords.shape[4] != 3:
+        raise RuntimeError(f"coord_volumes must be (B, Vx, Vy, Vz, 3), got {tuple(coords.shape)}")
+    if conf is not None and conf.shape != feat.shape[:3]:
+        raise RuntimeError(f"vol_confidences must be {tuple(feat.shape[:3])}, got {tuple(conf.shape)}")
+    od = _dtype_code(out_dtype if out_dtype is not None else feat.dtype)
+    return UnprojectFunction.apply(feat, proj, coords, conf, agg, bool(align_corners), od)
+
+
+def integrate_tensor_3d_with_coordinates(volumes, coord_volumes, softmax=True, *, multiplier=1.0,
+                                         return_volumes=True, out_dtype=None):
+    """3D soft-argmax: returns (coordinates (B, J, 3), normalised volumes (B, J, Vx, Vy, Vz)).
+
+    Reference: ``mvn/utils/op.py:84-96``.  ``multiplier`` fuses the caller's
+    ``volumes * volume_multiplier`` (triangulation.py:353).  With ``softmax=False``
+    the reference applies relu and does NOT normalise the mass (op.py:91); so do we.
+    """
+    vol = volumes
+    if vol.dtype not in (torch.float32, torch.bfloat16):
+        vol = vol.float()
+    if vol.dim() != 5:
+        raise RuntimeError(f"volumes must be (B, J, Vx, Vy, Vz), got {tuple(vol.shape)}")
+    Vx, Vy, Vz = vol.shape[2:]
+    if vol.stride(4) != 1 or vol.stride(3) != Vz or vol.stride(2) != Vy * Vz:
+        vol = vol.contiguous()
+    coords = coord_volumes.float().contiguous()
+    if coords.shape != (vol.shape[0], Vx, Vy, Vz, 3):
+        raise RuntimeError(f"coord_volumes {tuple(coords.shape)} does not match volumes {tuple(vol.shape)}")
+    od = _dtype_code(out_dtype if out_dtype is not None else vol.dtype)
+    xyz, out = SoftArgmaxFunction.apply(vol, coords, bool(softmax), float(multiplier), bool(return_volumes), od)
+    return xyz, (out if return_volumes else None)
+
+
+class UnprojectFunction(torch.autograd.Function):
+    """autograd surface of op.py:99-163 (backward kernels: see mvn_rocm/_backward.py)."""
+
+    @staticmethod
+    def forward(ctx, feat, proj, coords, conf, agg, align_corners, out_dtype):
+        out = _ops.unproject(feat, proj, coords, conf, agg, align_corners, out_dtype)
+        ctx.save_for_backward(feat, proj, coords, conf, out)
+        ctx.cfg = (agg, align_corners)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        from . import _backward
+        return _backward.unproject_backward(ctx, grad_out)
+
+
+class SoftArgmaxFunction(torch.autograd.Function):
+    """autograd surface of op.py:84-96."""
+
+    @staticmethod
+    def forward(ctx, vol, coords, softmax, multiplier, return_volume, out_dtype):
+        xyz, out = _ops.softargmax3d(vol, coords, softmax, multiplier, return_volume, out_dtype)
+        ctx.save_for_backward(vol, coords, xyz, out)
+        ctx.cfg = (softmax, multiplier, return_volume)
+        return xyz, out
+
+    @staticmethod
+    def backward(ctx, grad_xyz, grad_out):
+        from . import _backward
+        return _backward.softargmax_backward(ctx, grad_xyz, grad_out)

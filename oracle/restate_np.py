@@ -1,0 +1,40 @@
+"""ORACLE — test infrastructure only.
+
+float64 restatement of the confidence-weighted DLT (mvn/utils/multiview.py:132-174).
+The design matrix is formed in float32 with the reference's three separately rounded
+ops (multiview.py:150-152) and only the null-space solve is promoted to float64
+(LAPACK gesdd via numpy).  This is the gate for the HIP DLT (<= 1e-6 relative): the
+float32 reference SVD itself is ~2e-4 away from float64 on realistic cameras
+(SURVEY.md §7, Appendix A), so no float32 ordering could meet 1e-4 against it.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def design_matrix(P: np.ndarray, pts: np.ndarray, conf) -> np.ndarray:
+    """P (N,3,4), pts (N,2), conf (N,) or None -> A (2N,4) float32."""
+    P = np.asarray(P, np.float32)
+    pts = np.asarray(pts, np.float32)
+    n = P.shape[0]
+    c = np.ones(n, np.float32) if conf is None else np.asarray(conf, np.float32)
+    A = np.broadcast_to(P[:, 2:3, :], (n, 2, 4)) * pts.reshape(n, 2, 1)   # :150
+    A = A - P[:, :2, :]                                                   # :151
+    A = A * c.reshape(-1, 1, 1)                                           # :152
+    return A.reshape(-1, 4).astype(np.float32)
+
+
+def triangulate_batch_of_points(proj, points, confidences=None) -> np.ndarray:
+    """proj (B,N,3,4), points (B,N,J,2), confidences (B,N,J) -> (B,J,3) float64."""
+    proj = np.asarray(proj)
+    points = np.asarray(points)
+    B, N, J = points.shape[:3]
+    out = np.zeros((B, J, 3), np.float64)
+    for b in range(B):
+        for j in range(J):
+            conf = None if confidences is None else np.asarray(confidences)[b, :, j]
+            A = design_matrix(proj[b], points[b, :, j], conf).astype(np.float64)
+            _, _, vh = np.linalg.svd(A, full_matrices=False)
+            X = vh[-1]
+            out[b, j] = X[:3] / X[3]
+    return out

@@ -1,0 +1,111 @@
+"""C ABI of libmvn_hip.so and the host-side checks of mvn_rocm — no GPU needed
+(only argument-validation paths are called; they return before any HIP call)."""
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "mvn_hip.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(mvn_\w+)\s*\(", text, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from mvn_rocm import _lib
+    return _lib.load()
+
+
+def test_header_declares_the_three_entry_points():
+    fns = header_functions()
+    for name in ("mvn_unproject", "mvn_softargmax3d", "mvn_dlt", "mvn_softargmax3d_workspace_bytes",
+                 "mvn_strerror", "mvn_version"):
+        assert name in fns
+
+
+def test_every_declared_symbol_is_exported(lib):
+    from mvn_rocm import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT\s+(mvn_\w+)", out))
+    for name in header_functions():
+        assert name in exported, name
+        assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
+        getattr(lib, name)
+
+
+def test_version_and_errors(lib):
+    assert lib.mvn_version() == (0 << 16) | (1 << 8)
+    for code in (0, -1, -2, -3, -4, -5):
+        assert lib.mvn_strerror(code)
+    assert lib.mvn_strerror(-99) == b"unknown error"
+
+
+def _unproject(lib, **kw):
+    a = dict(feat=1, fdt=0, proj=1, coords=1, conf=None, out=1, odt=0, B=1, N=4, C=32, H=96, W=96,
+             Vx=64, Vy=64, Vz=64, agg=2, ac=0)
+    a.update(kw)
+    return lib.mvn_unproject(a["feat"], a["fdt"], a["proj"], a["coords"], a["conf"], a["out"], a["odt"],
+                             a["B"], a["N"], a["C"], a["H"], a["W"], a["Vx"], a["Vy"], a["Vz"], a["agg"], a["ac"],
+                             None)
+
+
+def test_unproject_argument_validation(lib):
+    assert _unproject(lib, feat=None) == -1
+    assert _unproject(lib, agg=7) == -1
+    assert _unproject(lib, agg=3, conf=None) == -1          # 'conf' aggregation needs confidences
+    assert _unproject(lib, ac=2) == -1
+    assert _unproject(lib, B=0) == -2
+    assert _unproject(lib, W=-1) == -2
+    assert _unproject(lib, Vx=2048, Vy=2048, Vz=2048) == -2
+    assert _unproject(lib, fdt=0, odt=1) == -3               # f32 features -> bf16 volume unsupported
+
+
+def test_softargmax_argument_validation(lib):
+    ws = lib.mvn_softargmax3d_workspace_bytes(32, 17, 64, 64, 64)
+    assert ws == 32 * 17 * 64 * 5 * 4
+    assert lib.mvn_softargmax3d_workspace_bytes(0, 17, 64, 64, 64) == 0
+    call = lambda **k: lib.mvn_softargmax3d(
+        k.get("vol", 1), 0, 17 * 64 ** 3, 64 ** 3, 1, 1.0, k.get("sm", 1), 1, None, 0, k.get("ws", 1),
+        k.get("wsb", ws), 32, 17, 64, 64, 64, None)
+    assert call(vol=None) == -1
+    assert call(sm=3) == -1
+    assert call(ws=None) == -5
+    assert call(wsb=ws - 4) == -5
+
+
+def test_dlt_argument_validation(lib):
+    assert lib.mvn_dlt(None, 1, None, 1, 1, 4, 17, None) == -1
+    assert lib.mvn_dlt(1, 1, None, 1, 1, 0, 17, None) == -2
+
+
+def test_python_api_has_no_cpu_fallback():
+    from mvn_rocm import op, multiview
+    feat = torch.zeros(1, 2, 3, 8, 8)
+    P = torch.zeros(1, 2, 3, 4)
+    coords = torch.zeros(1, 4, 4, 4, 3)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        op.unproject_heatmaps(feat, P, coords, "softmax")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        op.integrate_tensor_3d_with_coordinates(torch.zeros(1, 2, 4, 4, 4), coords)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        multiview.triangulate_batch_of_points(P, torch.zeros(1, 2, 5, 2))
+
+
+def test_python_api_error_types_match_reference():
+    from mvn_rocm import op, multiview
+    feat = torch.zeros(1, 2, 3, 8, 8)
+    P = torch.zeros(1, 2, 3, 4)
+    coords = torch.zeros(1, 4, 4, 4, 3)
+    with pytest.raises(ValueError, match="Unknown volume_aggregation_method: mean"):   # op.py:161
+        op.unproject_heatmaps(feat, P, coords, "mean")
+    with pytest.raises(AssertionError):                                                # multiview.py:143
+        multiview.triangulate_batch_of_points(torch.zeros(1, 3, 3, 4), torch.zeros(1, 2, 5, 2))
+    assert op.aggregation_code("conf_norm") == op.aggregation_code("conf")             # op.py:147

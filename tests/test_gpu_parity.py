@@ -1,0 +1,246 @@
+"""HIP kernels vs the oracle and the reference's golden vectors (MI355X only).
+
+Bars (BASELINE.json north_star):
+  unproject 'sum' / 'max' / 'conf' : bit-exact (same f32 op order as ATen CPU)
+  unproject 'softmax'              : max-rel <= 1e-5 (exp rounding only; target 1e-4)
+  soft-argmax                      : max-rel <= 1e-5 on coordinates and volumes
+  DLT                              : max-rel <= 1e-6 vs the float64 restatement
+  bf16                             : f32 reference on bf16-rounded features, output
+                                     rounded to bf16 -> <= 1 bf16 ulp (2^-8 rel)
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import max_rel
+from oracle import capi, restate_np
+
+pytestmark = pytest.mark.gpu
+
+METHODS = ("sum", "max", "softmax", "conf")
+
+
+def _op():
+    from mvn_rocm import op
+    return op
+
+
+def _t(a, device, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    return t if dtype is None else t.to(dtype)
+
+
+def bf16_to_f32(bits):
+    return (np.asarray(bits, np.uint32) << 16).view(np.float32)
+
+
+def assert_unproject_parity(out, ref, method, tol=1e-5):
+    if method == "softmax":
+        assert max_rel(out, ref) <= tol
+    else:
+        np.testing.assert_array_equal(out, ref)
+
+
+# ----------------------------------------------------------------------------- unproject
+@pytest.mark.parametrize("method", METHODS)
+@pytest.mark.parametrize("ac", (0, 1))
+def test_unproject_matches_reference_golden(golden, device, method, ac):
+    d = golden("unproject_small.npz")
+    out = _op().unproject_heatmaps(_t(d["feat"], device), _t(d["proj"], device), _t(d["coords"], device), method,
+                                   _t(d["conf"], device), align_corners=bool(ac))
+    assert out.dtype == torch.float32 and out.shape == (2, 5, 8, 9, 10)
+    assert_unproject_parity(out.cpu().numpy(), d[f"{method}_ac{ac}"], method)
+
+
+@pytest.mark.parametrize("method", ("sum", "softmax"))
+def test_unproject_bf16_matches_reference_golden(golden, device, method):
+    d = golden("unproject_small.npz")
+    feat = _t(d["feat"], device).to(torch.bfloat16)
+    ref = d[f"bf16in_{method}_ac0"]
+    out32 = _op().unproject_heatmaps(feat, _t(d["proj"], device), _t(d["coords"], device), method,
+                                     out_dtype=torch.float32)
+    assert_unproject_parity(out32.cpu().numpy(), ref, method)
+    out16 = _op().unproject_heatmaps(feat, _t(d["proj"], device), _t(d["coords"], device), method)
+    assert out16.dtype == torch.bfloat16
+    np.testing.assert_allclose(out16.float().cpu().numpy(), ref, rtol=2 ** -8, atol=2 ** -8 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("method", ("sum", "softmax"))
+def test_unproject_config_slice_golden(golden, device, method):
+    d = golden("unproject_cfg.npz")
+    out = _op().unproject_heatmaps(_t(d["feat"], device), _t(d["proj"], device), _t(d["coords"], device), method)
+    assert_unproject_parity(out.cpu().numpy(), d[f"{method}_ac0"], method)
+
+
+@pytest.mark.parametrize("n_views", (1, 2, 3, 5, 8, 9, 12))
+@pytest.mark.parametrize("method", METHODS)
+def test_unproject_random_shapes_vs_oracle(device, n_views, method):
+    from mvn_rocm import synth
+    rng = np.random.default_rng(100 + n_views)
+    B, C, H, W = 2, 3, 13, 19
+    vb = synth.volumetric_batch(B, n_views=n_views, channels=C, heatmap=max(H, W), volume=12, seed=n_views)
+    feat = rng.standard_normal((B, n_views, C, H, W)).astype(np.float32)
+    proj = vb.proj.numpy()
+    proj[:, :, 0] *= W / max(H, W)
+    proj[:, :, 1] *= H / max(H, W)
+    coords = vb.coords.numpy()[:, :12, :11, :10]          # non-cubic volume
+    conf = rng.uniform(0.0, 1.0, (B, n_views, C)).astype(np.float32)
+    for ac in (False, True):
+        ref = capi.unproject(feat, proj, coords, method, conf, ac)
+        out = _op().unproject_heatmaps(_t(feat, device), _t(proj, device), _t(coords, device), method,
+                                       _t(conf, device), align_corners=ac)
+        assert_unproject_parity(out.cpu().numpy(), ref, method)
+
+
+@pytest.mark.parametrize("method", ("softmax", "sum"))
+def test_unproject_full_config_frame_vs_oracle(device, method):
+    """One frame of BASELINE config 2 (4 views x 32 ch x 96^2 -> 64^3)."""
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(1, seed=21)
+    ref = capi.unproject(vb.features.numpy(), vb.proj.numpy(), vb.coords.numpy(), method)
+    out = _op().unproject_heatmaps(vb.features.to(device), vb.proj.to(device), vb.coords.to(device), method)
+    assert_unproject_parity(out.cpu().numpy(), ref, method)
+    assert 0.2 < (ref != 0).mean()          # the cuboid really projects into the maps
+
+
+def test_unproject_full_size_properties(device):
+    """Batch-32 properties the oracle cannot afford at full size: linearity of 'sum'
+    in the features, view-permutation invariance, frame independence."""
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(32, dtype=torch.float32, device=device, seed=4)
+    op = _op()
+    f, P, X = vb.features, vb.proj, vb.coords
+    a = op.unproject_heatmaps(f, P, X, "sum")
+    b = op.unproject_heatmaps(2.0 * f, P, X, "sum")
+    torch.testing.assert_close(b, 2.0 * a, rtol=0, atol=0)         # scaling by 2 is exact
+    perm = torch.tensor([2, 0, 3, 1], device=device)
+    s1 = op.unproject_heatmaps(f, P, X, "softmax")
+    s2 = op.unproject_heatmaps(f[:, perm], P[:, perm], X, "softmax")
+    assert max_rel(s2.cpu().numpy(), s1.cpu().numpy()) <= 1e-6
+    one = op.unproject_heatmaps(f[7:8], P[7:8], X[7:8], "softmax")
+    torch.testing.assert_close(one[0], s1[7], rtol=0, atol=0)      # frames are independent
+    assert torch.isfinite(s1).all()
+
+
+# ----------------------------------------------------------------------------- soft-argmax
+@pytest.mark.parametrize("softmax", (True, False))
+@pytest.mark.parametrize("mult", (1.0, 1.7))
+def test_softargmax_matches_reference_golden(golden, device, softmax, mult):
+    d = golden("softargmax_small.npz")
+    key = f"sm{int(softmax)}_m{mult}"
+    xyz, vol = _op().integrate_tensor_3d_with_coordinates(_t(d["vol"], device), _t(d["coords"], device),
+                                                          softmax, multiplier=mult)
+    assert max_rel(xyz.cpu().numpy(), d[f"xyz_{key}"]) <= 1e-5
+    assert max_rel(vol.cpu().numpy(), d[f"vol_{key}"]) <= 1e-5
+
+
+def test_softargmax_blob_golden(golden, device):
+    d = golden("softargmax_blob.npz")
+    xyz, vol = _op().integrate_tensor_3d_with_coordinates(_t(d["vol"], device), _t(d["coords"], device))
+    assert max_rel(xyz.cpu().numpy(), d["xyz"]) <= 1e-5
+    assert max_rel(vol.cpu().numpy(), d["vol_out"]) <= 1e-5
+
+
+@pytest.mark.parametrize("softmax", (True, False))
+def test_softargmax_full_size_vs_oracle(device, softmax):
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(2, channels=1, seed=8)
+    vol = synth.blob_volumes(vb.coords, 17, seed=8)
+    ref_xyz, ref_vol = capi.softargmax3d(vol.numpy(), vb.coords.numpy(), softmax, 1.0)
+    xyz, out = _op().integrate_tensor_3d_with_coordinates(vol.to(device), vb.coords.to(device), softmax)
+    assert max_rel(xyz.cpu().numpy(), ref_xyz) <= 1e-5
+    assert max_rel(out.cpu().numpy(), ref_vol) <= 1e-5
+
+
+def test_softargmax_channel_slice_and_bf16(device):
+    """The bench feeds channels [0:17] of a (B, 32, V^3) unprojection without a copy."""
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(2, channels=1, volume=32, seed=9)
+    big = torch.randn((2, 32, 32, 32, 32), generator=torch.Generator().manual_seed(3)) * 4
+    sl = big.to(device)[:, :17]
+    assert not sl.is_contiguous()
+    ref_xyz, ref_vol = capi.softargmax3d(big[:, :17].numpy(), vb.coords.numpy(), True, 1.3)
+    xyz, out = _op().integrate_tensor_3d_with_coordinates(sl, vb.coords.to(device), multiplier=1.3)
+    assert max_rel(xyz.cpu().numpy(), ref_xyz) <= 1e-5
+    assert max_rel(out.cpu().numpy(), ref_vol) <= 1e-5
+    # bf16 volume: oracle on the bf16-rounded logits, bf16 output within 1 ulp
+    sl16 = sl.to(torch.bfloat16)
+    ref_xyz, ref_vol = capi.softargmax3d(sl16.float().cpu().numpy(), vb.coords.numpy(), True, 1.3)
+    xyz, out = _op().integrate_tensor_3d_with_coordinates(sl16, vb.coords.to(device), multiplier=1.3)
+    assert out.dtype == torch.bfloat16
+    assert max_rel(xyz.cpu().numpy(), ref_xyz) <= 1e-5
+    np.testing.assert_allclose(out.float().cpu().numpy(), ref_vol, rtol=2 ** -8, atol=1e-30)
+    xyz2, none = _op().integrate_tensor_3d_with_coordinates(sl16, vb.coords.to(device), multiplier=1.3,
+                                                            return_volumes=False)
+    assert none is None
+    torch.testing.assert_close(xyz2, xyz, rtol=0, atol=0)
+
+
+def test_softargmax_translation_equivariance(device):
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(4, channels=1, device=device, seed=10)
+    vol = synth.blob_volumes(vb.coords, 17, seed=10)
+    shift = torch.tensor([123.5, -77.25, 10.0], device=device)
+    a, _ = _op().integrate_tensor_3d_with_coordinates(vol, vb.coords)
+    b, _ = _op().integrate_tensor_3d_with_coordinates(vol, vb.coords + shift)
+    torch.testing.assert_close(b, a + shift, rtol=0, atol=2e-3)
+
+
+# ----------------------------------------------------------------------------- DLT
+@pytest.mark.parametrize("case", ("cfg1", "b3n3", "n8"))
+@pytest.mark.parametrize("use_conf", (True, False))
+def test_dlt_matches_float64_restatement(golden, device, case, use_conf):
+    from mvn_rocm import multiview
+    d = golden("dlt.npz")
+    key = f"{case}_c{int(use_conf)}"
+    conf = d[f"conf_{case}"] if use_conf else None
+    out = multiview.triangulate_batch_of_points(_t(d[f"proj_{case}"], device), _t(d[f"points_{case}"], device),
+                                                None if conf is None else _t(conf, device)).cpu().numpy()
+    x64 = restate_np.triangulate_batch_of_points(d[f"proj_{case}"], d[f"points_{case}"], conf)
+    assert max_rel(out, x64) <= 1e-6
+    assert max_rel(out, d[f"out64_{key}"]) <= 2e-6
+    assert max_rel(out, d[f"out_{key}"]) <= 1e-3      # the float32 reference's own SVD error
+
+
+def test_dlt_many_views_and_degenerate_confidences(device):
+    from mvn_rocm import multiview, synth
+    ab = synth.algebraic_batch(4, n_views=31, n_joints=17, seed=5)
+    conf = ab.confidences.clone()
+    conf[:, 5:20] = 0.0                  # zero-confidence views contribute nothing
+    out = multiview.triangulate_batch_of_points(ab.proj.to(device), ab.points.to(device), conf.to(device))
+    x64 = restate_np.triangulate_batch_of_points(ab.proj.numpy(), ab.points.numpy(), conf.numpy())
+    assert max_rel(out.cpu().numpy(), x64) <= 1e-6
+    # noise-free points reproduce the ground truth
+    ab0 = synth.algebraic_batch(2, n_views=4, n_joints=17, seed=6, noise_px=0.0)
+    out = multiview.triangulate_batch_of_points(ab0.proj.to(device), ab0.points.to(device))
+    assert np.abs(out.cpu().numpy() - ab0.points_3d.numpy()).max() < 0.5     # mm; f32 pixel rounding
+
+
+def test_dlt_single_point_api(device):
+    from mvn_rocm import multiview, synth
+    ab = synth.algebraic_batch(1, 4, 3, seed=7)
+    one = multiview.triangulate_point_from_multiple_views_linear_torch(
+        ab.proj[0].to(device), ab.points[0, :, 1].to(device), ab.confidences[0, :, 1].to(device))
+    batch = multiview.triangulate_batch_of_points(ab.proj.to(device), ab.points.to(device), ab.confidences.to(device))
+    torch.testing.assert_close(one, batch[0, 1], rtol=0, atol=0)
+
+
+# ----------------------------------------------------------------------------- plumbing
+def test_ops_follow_the_current_stream(device):
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(2, volume=16, device=device, seed=12)
+    ref = _op().unproject_heatmaps(vb.features, vb.proj, vb.coords, "softmax")
+    s = torch.cuda.Stream(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        out = _op().unproject_heatmaps(vb.features, vb.proj, vb.coords, "softmax")
+    torch.cuda.current_stream(device).wait_stream(s)
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
+
+
+def test_hip_library_is_the_one_loaded():
+    """The product path must run libmvn_hip.so from this tree, not a fallback."""
+    from mvn_rocm import _lib
+    _lib.load()
+    maps = open("/proc/self/maps").read()
+    assert _lib.LIB_PATH in maps

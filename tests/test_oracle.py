@@ -1,0 +1,120 @@
+"""The oracle itself, pinned against vectors captured from the reference (CPU only)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import max_rel
+from oracle import capi, restate_np, restate_torch
+
+METHODS = ("sum", "max", "softmax", "conf")
+
+
+@pytest.mark.parametrize("method", METHODS)
+@pytest.mark.parametrize("ac", (0, 1))
+def test_c_oracle_unproject_small(golden, method, ac):
+    d = golden("unproject_small.npz")
+    ref = d[f"{method}_ac{ac}"]
+    out = capi.unproject(d["feat"], d["proj"], d["coords"], method, d["conf"], bool(ac))
+    if method == "softmax":     # expf rounding differs from ATen's vectorised exp
+        assert max_rel(out, ref) <= 1e-6
+    else:                       # bit-exact recipe
+        np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("method", ("sum", "softmax"))
+def test_c_oracle_unproject_bf16_input(golden, method):
+    d = golden("unproject_small.npz")
+    out = capi.unproject(d["feat_bf16_bits"], d["proj"], d["coords"], method, None, False, feat_bf16_bits=True)
+    ref = d[f"bf16in_{method}_ac0"]
+    if method == "sum":
+        np.testing.assert_array_equal(out, ref)
+    else:
+        assert max_rel(out, ref) <= 1e-6
+
+
+@pytest.mark.parametrize("method", ("sum", "softmax"))
+def test_c_oracle_unproject_cfg_slice(golden, method):
+    d = golden("unproject_cfg.npz")
+    out = capi.unproject(d["feat"], d["proj"], d["coords"], method)
+    ref = d[f"{method}_ac0"]
+    if method == "sum":
+        np.testing.assert_array_equal(out, ref)
+    else:
+        assert max_rel(out, ref) <= 1e-6
+
+
+def test_golden_exercises_edge_cases(golden):
+    """The small fixture must contain behind-camera voxels, exact-zero depth and
+    out-of-bounds taps, or the bit-exact claims above prove little."""
+    d = golden("unproject_small.npz")
+    P, X = d["proj"].astype(np.float64), d["coords"].reshape(2, -1, 3).astype(np.float64)
+    Xh = np.concatenate([X, np.ones(X.shape[:2] + (1,))], -1)
+    w = np.einsum("bvk,bnk->bvn", P[:, :, 2, :], Xh)
+    assert (w < 0).any() and (w == 0).any() and (w > 0).any()
+    # some (frame, view) pairs leave voxels with nothing sampled (behind / out of bounds)
+    zero_frac = [(capi.unproject(d["feat"][:, v:v + 1], d["proj"][:, v:v + 1], d["coords"], "sum")[b] == 0).mean()
+                 for v in range(d["feat"].shape[1]) for b in range(2)]
+    assert max(zero_frac) > 0.5 and min(zero_frac) < 0.5
+
+
+@pytest.mark.parametrize("method", METHODS)
+def test_torch_restatement_is_bit_exact(golden, method):
+    d = golden("unproject_small.npz")
+    for ac in (0, 1):
+        out = restate_torch.unproject_heatmaps(
+            torch.from_numpy(d["feat"]), torch.from_numpy(d["proj"]), torch.from_numpy(d["coords"]), method,
+            torch.from_numpy(d["conf"]), align_corners=bool(ac)).numpy()
+        np.testing.assert_array_equal(out, d[f"{method}_ac{ac}"])
+
+
+def test_torch_restatement_rejects_unknown_aggregation(golden):
+    d = golden("unproject_small.npz")
+    with pytest.raises(ValueError, match="Unknown volume_aggregation_method"):
+        restate_torch.unproject_heatmaps(torch.from_numpy(d["feat"]), torch.from_numpy(d["proj"]),
+                                         torch.from_numpy(d["coords"]), "mean")
+
+
+@pytest.mark.parametrize("softmax", (True, False))
+@pytest.mark.parametrize("mult", (1.0, 1.7))
+def test_softargmax_oracles(golden, softmax, mult):
+    d = golden("softargmax_small.npz")
+    key = f"sm{int(softmax)}_m{mult}"
+    xyz, vol = capi.softargmax3d(d["vol"], d["coords"], softmax, mult)
+    assert max_rel(xyz, d[f"xyz_{key}"]) <= 5e-6   # f32 reference vs f64 oracle (1.3e-6)
+    assert max_rel(vol, d[f"vol_{key}"]) <= 1e-6
+    v = torch.from_numpy(d["vol"]) * mult
+    txyz, tvol = restate_torch.integrate_tensor_3d_with_coordinates(v, torch.from_numpy(d["coords"]), softmax)
+    np.testing.assert_array_equal(txyz.numpy(), d[f"xyz_{key}"])
+    np.testing.assert_array_equal(tvol.numpy(), d[f"vol_{key}"])
+
+
+def test_softargmax_oracle_blob(golden):
+    d = golden("softargmax_blob.npz")
+    xyz, vol = capi.softargmax3d(d["vol"], d["coords"], True, 1.0)
+    assert max_rel(xyz, d["xyz"]) <= 1e-6
+    assert max_rel(vol, d["vol_out"]) <= 1e-6
+
+
+@pytest.mark.parametrize("case", ("cfg1", "b3n3", "n8"))
+@pytest.mark.parametrize("use_conf", (True, False))
+def test_dlt_oracles(golden, case, use_conf):
+    d = golden("dlt.npz")
+    key = f"{case}_c{int(use_conf)}"
+    conf = d[f"conf_{case}"] if use_conf else None
+    # torch restatement reproduces the float32 reference bit-for-bit
+    t = restate_torch.triangulate_batch_of_points(torch.from_numpy(d[f"proj_{case}"]),
+                                                  torch.from_numpy(d[f"points_{case}"]),
+                                                  None if conf is None else torch.from_numpy(conf)).numpy()
+    np.testing.assert_array_equal(t, d[f"out_{key}"])
+    # float64 restatement: agrees with the reference's own float64 re-run
+    x64 = restate_np.triangulate_batch_of_points(d[f"proj_{case}"], d[f"points_{case}"], conf)
+    assert max_rel(x64, d[f"out64_{key}"]) <= 2e-6
+    # ... and the float32 reference is within its known conditioning error of it
+    assert max_rel(d[f"out_{key}"], x64) <= 1e-3
+    # design matrix: C restatement == numpy restatement, bit for bit
+    for b in range(d[f"points_{case}"].shape[0]):
+        for j in range(0, d[f"points_{case}"].shape[2], 4):
+            a_c = capi.dlt_design(d[f"proj_{case}"], d[f"points_{case}"], conf, b, j)
+            a_n = restate_np.design_matrix(d[f"proj_{case}"][b], d[f"points_{case}"][b, :, j],
+                                           None if conf is None else conf[b, :, j])
+            np.testing.assert_array_equal(a_c, a_n)

@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from mvn_rocm import op, synth  # noqa: E402
+from mvn_rocm import dist as mdist, op, synth  # noqa: E402
 
 METRIC = "multiview frames/sec (4-view x 64^3 unproject+soft-argmax), 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -69,7 +69,6 @@ class Workload:
                                     volume=cfg["volume"], dtype=cfg["dtype"], device=device, seed=seed,
                                     first_frame=rank * B)
         self.feat, self.proj, self.coords = vb.features, vb.proj, vb.coords
-        self.gathered = torch.empty((world * B, cfg["joints"], 3), device=device) if world > 1 else None
         self.ev = []
 
     def step(self, timed=False):
@@ -82,8 +81,8 @@ class Workload:
             e1.record()
             self.ev.append((e0, e1))
         xyz, sm = op.integrate_tensor_3d_with_coordinates(vol[:, :J], self.coords, True)
-        if self.gathered is not None:
-            dist.all_gather_into_tensor(self.gathered, xyz)
+        if self.world > 1:      # the path's one exchange: joints of every rank, RCCL over xGMI
+            xyz = mdist.gather_joints(xyz, self.cfg["frames"] * self.world)
         return xyz, sm
 
     def unproject_ms(self):

@@ -41,4 +41,16 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
 
+// XCD-aware block order (cdna_hip_programming.md §5.5 T1, bijective form): hardware deals
+// blocks round-robin over the 8 XCDs, so block b runs on XCD b % 8.  Remapping gives each
+// XCD one contiguous range of logical work items, which keeps a frame's feature maps in
+// one XCD's L2 and lets neighbouring tiles' partial output lines merge there.  Speed only:
+// any placement computes the same result.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  constexpr int kXcd = 8;
+  const int q = nblk / kXcd, r = nblk % kXcd;
+  const int xcd = bid % kXcd, k = bid / kXcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
 }  // namespace mvn

@@ -14,73 +14,17 @@
 //   sampling    fma(v_se,se, fma(v_sw,sw, fma(v_ne,ne, v_nw*nw)))  (ATen CPU grid sampler, §8a a1.5)
 // so 'sum' / 'max' / 'conf' are bit-exact with the torch CPU reference and
 // 'softmax' differs only by exp() rounding (<= 1e-6 rel).
-#include "common.hpp"
+#include <stdlib.h>
+
+#include "unproject_common.hpp"
 
 namespace mvn {
 namespace {
 
+using namespace unproj;
+
 constexpr int kUnprojBlock = 256;
 constexpr int kMaxRegViews = 8;   // views whose geometry is held in registers
-
-// Bilinear taps of one voxel in one view: 4 clamped plane offsets + 4 weights.
-// Out-of-bounds corners and invalid (behind-camera) voxels get weight 0, which is
-// bit-identical to the reference's zero-valued corner / zeroed sample for finite
-// feature values (fma(v, 0, acc) == acc).
-struct Taps {
-  int o0, o1, o2, o3;
-  float w0, w1, w2, w3;
-};
-
-__device__ __forceinline__ Taps view_taps(const float* __restrict__ Pv, float x, float y, float z,
-                                          int H, int W, int align_corners) {
-  // op.py:117-119 -> multiview.py:96   [x y z 1] @ P^T
-  const float uh = __builtin_fmaf(1.f, Pv[3], __builtin_fmaf(z, Pv[2], __builtin_fmaf(y, Pv[1], x * Pv[0])));
-  const float vh = __builtin_fmaf(1.f, Pv[7], __builtin_fmaf(z, Pv[6], __builtin_fmaf(y, Pv[5], x * Pv[4])));
-  float wh = __builtin_fmaf(1.f, Pv[11], __builtin_fmaf(z, Pv[10], __builtin_fmaf(y, Pv[9], x * Pv[8])));
-  const bool invalid = wh <= 0.f;          // op.py:121, taken before the guard
-  if (wh == 0.f) wh = 1.f;                 // op.py:123
-  const float u = uh / wh;                 // multiview.py:75 (IEEE division)
-  const float v = vh / wh;
-  // op.py:128-129 — x is divided by heatmap_shape[0] (H) and y by [1] (W): reference quirk kept.
-  const float gx = 2.f * (u / float(H) - 0.5f);
-  const float gy = 2.f * (v / float(W) - 0.5f);
-  // grid_sample unnormalisation; x indexes W, y indexes H.
-  float ix, iy;
-  if (align_corners) {
-    ix = (gx + 1.f) * (float(W - 1) * 0.5f);
-    iy = (gy + 1.f) * (float(H - 1) * 0.5f);
-  } else {
-    // ATen: (g + 1) * (size / 2) - 0.5, contracted to one fma
-    ix = __builtin_fmaf(gx + 1.f, float(W) * 0.5f, -0.5f);
-    iy = __builtin_fmaf(gy + 1.f, float(H) * 0.5f, -0.5f);
-  }
-  const float fx0 = floorf(ix), fy0 = floorf(iy);
-  const float tx = ix - fx0, sx = 1.f - tx;
-  const float ty = iy - fy0, sy = 1.f - ty;
-  // corner validity in float (robust to huge / non-finite coordinates)
-  const bool x0in = (fx0 >= 0.f) & (fx0 < float(W));
-  const bool x1in = (fx0 >= -1.f) & (fx0 < float(W - 1));
-  const bool y0in = (fy0 >= 0.f) & (fy0 < float(H));
-  const bool y1in = (fy0 >= -1.f) & (fy0 < float(H - 1));
-  const bool ok = !invalid;
-  const int x0 = x0in ? int(fx0) : 0, x1 = x1in ? int(fx0) + 1 : 0;
-  const int y0 = y0in ? int(fy0) : 0, y1 = y1in ? int(fy0) + 1 : 0;
-  Taps t;
-  t.o0 = y0 * W + x0;  t.w0 = (ok & y0in & x0in) ? sy * sx : 0.f;   // nw
-  t.o1 = y0 * W + x1;  t.w1 = (ok & y0in & x1in) ? sy * tx : 0.f;   // ne
-  t.o2 = y1 * W + x0;  t.w2 = (ok & y1in & x0in) ? ty * sx : 0.f;   // sw
-  t.o3 = y1 * W + x1;  t.w3 = (ok & y1in & x1in) ? ty * tx : 0.f;   // se
-  return t;
-}
-
-template <typename TIn>
-__device__ __forceinline__ float sample(const TIn* __restrict__ plane, const Taps& t) {
-  const float a = to_f32(plane[t.o0]);
-  const float b = to_f32(plane[t.o1]);
-  const float c = to_f32(plane[t.o2]);
-  const float d = to_f32(plane[t.o3]);
-  return __builtin_fmaf(d, t.w3, __builtin_fmaf(c, t.w2, __builtin_fmaf(b, t.w1, a * t.w0)));
-}
 
 // ---- register-resident geometry, N <= 8 ----------------------------------
 template <int AGG, typename TIn, typename TOut>
@@ -184,9 +128,20 @@ __global__ __launch_bounds__(kUnprojBlock) void unproject_anyviews(
   }
 }
 
+// Kernel choice: the tiled LDS-staged kernel (unproject_tiled.hip) for N <= 8 views, the
+// register-geometry kernel above for MVN_UNPROJECT_KERNEL=simple (A/B and debugging), and
+// the any-N kernel for more than 8 views.
+inline bool use_simple_kernel() {
+  const char* e = getenv("MVN_UNPROJECT_KERNEL");
+  return e && e[0] == 's';
+}
+
 template <int AGG, typename TIn, typename TOut>
 int launch_agg(const void* feat, const float* P, const float* coords, const float* conf, void* out,
-               int B, int N, int C, int H, int W, int nvox, int align_corners, hipStream_t s) {
+               int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, hipStream_t s) {
+  const int nvox = Vx * Vy * Vz;
+  if (N <= kMaxRegViews && !use_simple_kernel())
+    return launch_tiled<AGG, TIn, TOut>(feat, P, coords, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
   dim3 grid((nvox + kUnprojBlock - 1) / kUnprojBlock, B);
   if (N <= kMaxRegViews)
     unproject_regviews<AGG, TIn, TOut><<<grid, kUnprojBlock, 0, s>>>(
@@ -201,17 +156,17 @@ int launch_agg(const void* feat, const float* P, const float* coords, const floa
 
 template <typename TIn, typename TOut>
 int launch_types(int agg, const void* feat, const float* P, const float* coords, const float* conf,
-                 void* out, int B, int N, int C, int H, int W, int nvox, int align_corners,
+                 void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners,
                  hipStream_t s) {
   switch (agg) {
     case MVN_AGG_SUM:
-      return launch_agg<MVN_AGG_SUM, TIn, TOut>(feat, P, coords, conf, out, B, N, C, H, W, nvox, align_corners, s);
+      return launch_agg<MVN_AGG_SUM, TIn, TOut>(feat, P, coords, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
     case MVN_AGG_MAX:
-      return launch_agg<MVN_AGG_MAX, TIn, TOut>(feat, P, coords, conf, out, B, N, C, H, W, nvox, align_corners, s);
+      return launch_agg<MVN_AGG_MAX, TIn, TOut>(feat, P, coords, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
     case MVN_AGG_SOFTMAX:
-      return launch_agg<MVN_AGG_SOFTMAX, TIn, TOut>(feat, P, coords, conf, out, B, N, C, H, W, nvox, align_corners, s);
+      return launch_agg<MVN_AGG_SOFTMAX, TIn, TOut>(feat, P, coords, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
     case MVN_AGG_CONF:
-      return launch_agg<MVN_AGG_CONF, TIn, TOut>(feat, P, coords, conf, out, B, N, C, H, W, nvox, align_corners, s);
+      return launch_agg<MVN_AGG_CONF, TIn, TOut>(feat, P, coords, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
   }
   return MVN_ERR_ARG;
 }
@@ -231,12 +186,11 @@ extern "C" int mvn_unproject(const void* feat, int feat_dtype, const float* proj
   const long long nvox = (long long)Vx * Vy * Vz;
   if (nvox > (1LL << 30) || (long long)H * W > (1LL << 30) || B > 65535) return MVN_ERR_SHAPE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int n = int(nvox);
   if (feat_dtype == MVN_DTYPE_F32 && out_dtype == MVN_DTYPE_F32)
-    return launch_types<float, float>(agg, feat, proj, coords, conf, out, B, N, C, H, W, n, align_corners, s);
+    return launch_types<float, float>(agg, feat, proj, coords, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
   if (feat_dtype == MVN_DTYPE_BF16 && out_dtype == MVN_DTYPE_BF16)
-    return launch_types<uint16_t, uint16_t>(agg, feat, proj, coords, conf, out, B, N, C, H, W, n, align_corners, s);
+    return launch_types<uint16_t, uint16_t>(agg, feat, proj, coords, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
   if (feat_dtype == MVN_DTYPE_BF16 && out_dtype == MVN_DTYPE_F32)
-    return launch_types<uint16_t, float>(agg, feat, proj, coords, conf, out, B, N, C, H, W, n, align_corners, s);
+    return launch_types<uint16_t, float>(agg, feat, proj, coords, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
   return MVN_ERR_DTYPE;
 }

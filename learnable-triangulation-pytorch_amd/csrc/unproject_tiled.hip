@@ -18,8 +18,10 @@
 // XCD-contiguously so a frame's maps stay in one XCD's L2 and z-neighbouring tiles
 // (which share output lines) run back to back on the same L2.
 //
-// A block whose footprints do not fit the LDS budget (a camera very close to the cuboid)
-// falls back to direct global gathers for that block only.
+// Footprints that do not fit the LDS budget together are staged in several passes; only a
+// single footprint larger than the whole budget sends its block to direct global gathers.
+#include <stdlib.h>
+
 #include "unproject_common.hpp"
 
 namespace mvn {
@@ -31,8 +33,8 @@ constexpr int kWaves = kThreads / kWave;
 constexpr int kSlots = 2048;          // 16-byte LDS pixel slots (32 KiB); slot 0 is a zero pad
 
 template <int NV> struct TileShape;                 // tile dims and voxels per thread
-template <> struct TileShape<4> { static constexpr int TX = 8, TY = 4, TZ = 16, VPT = 2; };
-template <> struct TileShape<8> { static constexpr int TX = 4, TY = 4, TZ = 16, VPT = 1; };
+template <> struct TileShape<4> { static constexpr int TX = 8, TY = 8, TZ = 8, VPT = 2; };
+template <> struct TileShape<8> { static constexpr int TX = 4, TY = 8, TZ = 8, VPT = 1; };
 
 // 16-byte slot <-> G floats
 __device__ __forceinline__ void unpack(const uint4& q, float (&v)[4]) {
@@ -93,7 +95,7 @@ template <int AGG, typename TIn, typename TOut, int NV>
 __global__ __launch_bounds__(kThreads) void unproject_tiled(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ conf, TOut* __restrict__ out, int B, int N, int C, int H, int W, int Vx,
-    int Vy, int Vz, int align_corners) {
+    int Vy, int Vz, int align_corners, int budget) {
   using S = TileShape<NV>;
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ, VPT = S::VPT;
   static_assert(TX * TY * TZ == kThreads * VPT, "tile must give every thread VPT voxels");
@@ -103,7 +105,9 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
   __shared__ int red[kWaves][NV][4];
   __shared__ int region[NV][4];                       // xs, ys, bw, first slot (-1: global fallback)
   __shared__ int region_end[NV];
+  __shared__ int region_pass[NV];
   __shared__ float region_inv_bw[NV];
+  __shared__ int block_info[1];                       // number of LDS passes, -1 = global fallback
 
   // ---- which tile (XCD-contiguous order, z-tiles fastest) -------------------------
   const int nTx = (Vx + TX - 1) / TX, nTy = (Vy + TY - 1) / TY, nTz = (Vz + TZ - 1) / TZ;
@@ -181,7 +185,11 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
   }
   __syncthreads();
   if (t == 0) {
-    int next = 1;                                     // slot 0 stays zero
+    // Pack the views' footprints into LDS passes (first fit in view order).  Normally all
+    // N views fit one pass; a close camera needs more passes, never a slow path.  Only a
+    // single footprint larger than the whole budget sends the block to global gathers.
+    int next = 1, pass = 0;                           // slot 0 stays a zero pad
+    bool too_big = false;
     for (int v = 0; v < NV; ++v) {
       if (v >= N) break;
       int x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN;
@@ -192,21 +200,19 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
       int bw = 0, bh = 0;
       if (x0 <= x1) { bw = x1 - x0 + 2; bh = y1 - y0 + 2; }   // +1 px for the east / south taps
       const long long area = (long long)bw * bh;
-      region[v][0] = x0; region[v][1] = y0; region[v][2] = bw;
-      if (next + area <= kSlots) {
-        region[v][3] = next;
-        region_end[v] = next + int(area);
-        next += int(area);
-      } else {
-        region[v][3] = -1;                            // footprint too large: direct gathers
-        region_end[v] = next;
-      }
+      if (area > budget - 1) too_big = true;
+      if (next + area > budget) { ++pass; next = 1; }
+      region[v][0] = x0; region[v][1] = y0; region[v][2] = bw; region[v][3] = next;
+      region_end[v] = next + int(area);
+      region_pass[v] = pass;
       region_inv_bw[v] = bw > 0 ? 1.f / float(bw) : 0.f;
+      next += int(area);
     }
+    block_info[0] = too_big ? -1 : pass + 1;
   }
   __syncthreads();
 
-  int rx[NV], ry[NV], rbw[NV], rbase[NV], rend[NV];
+  int rx[NV], ry[NV], rbw[NV], rbase[NV], rend[NV], rpass[NV];
   float rinv[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {       // block-uniform: keep in SGPRs
@@ -215,11 +221,24 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
     rbw[v] = __builtin_amdgcn_readfirstlane(region[v][2]);
     rbase[v] = __builtin_amdgcn_readfirstlane(region[v][3]);
     rend[v] = __builtin_amdgcn_readfirstlane(region_end[v]);
+    rpass[v] = __builtin_amdgcn_readfirstlane(region_pass[v]);
     rinv[v] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(region_inv_bw[v])));
   }
-  int total = 1;
+  const int npass = __builtin_amdgcn_readfirstlane(block_info[0]);
+
+  const TIn* fb = feat + size_t(b) * N * C * HW;
+  const float* cfb = conf ? conf + size_t(b) * N * C : nullptr;
+
+  if (npass < 0) {
+    // Pathological geometry (one view's footprint exceeds the whole LDS budget): the block
+    // gathers straight from global memory instead; same arithmetic and op order.
 #pragma unroll
-  for (int v = 0; v < NV; ++v) if (v < N) total = max(total, rend[v]);
+    for (int k = 0; k < VPT; ++k)
+      if (act[k])
+        gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + vox[k], nvox, N, C, H, W,
+                                     cx[k], cy[k], cz[k], align_corners);
+    return;
+  }
 
   // slot of each voxel-view's north-west tap
   int slot[NV][VPT];
@@ -229,58 +248,44 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
     for (int k = 0; k < VPT; ++k)
       slot[v][k] = rbase[v] + (fy[v][k] - ry[v]) * rbw[v] + (fx[v][k] - rx[v]);
 
-  const TIn* fb = feat + size_t(b) * N * C * HW;
-  const float* cfb = conf ? conf + size_t(b) * N * C : nullptr;
-
-  bool fits = true;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) fits &= (v >= N) | (rbase[v] >= 0);
-  if (!fits) {
-    // Rare (a camera very close to the cuboid): some footprint exceeds the LDS budget.
-    // The whole block gathers straight from global memory instead; same arithmetic.
-#pragma unroll
-    for (int k = 0; k < VPT; ++k)
-      if (act[k])
-        gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + vox[k], nvox, N, C, H, W,
-                                         cx[k], cy[k], cz[k], align_corners);
-    return;
-  }
-
   for (int c0 = 0; c0 < C; c0 += G) {
-    // ---- stage the footprints of all views for channels [c0, c0 + G) ------------
-    for (int idx = 1 + t; idx < total; idx += kThreads) {
-      int v = 0;
+    float sv[VPT][G][NV];
+    for (int pass = 0; pass < npass; ++pass) {
+      // ---- stage this pass's footprints for channels [c0, c0 + G) -----------------
+      int total = 1;
 #pragma unroll
-      for (int u = 1; u < NV; ++u)
-        if (u < N && rbase[u] >= 0 && idx >= rbase[u]) v = u;
-      const int li = idx - rbase[v];
-      const int py = int((float(li) + 0.5f) * rinv[v]);
-      const int px = li - py * rbw[v];
-      const int gx = rx[v] + px, gy = ry[v] + py;
-      const bool in = (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
-      const TIn* src = fb + (size_t(v) * C + c0) * HW + (in ? size_t(gy) * W + gx : 0);
-      uint32_t bits[G];
+      for (int v = 0; v < NV; ++v) if (v < N && rpass[v] == pass) total = max(total, rend[v]);
+      for (int idx = 1 + t; idx < total; idx += kThreads) {
+        int v = 0;
 #pragma unroll
-      for (int k = 0; k < G; ++k) bits[k] = (in && c0 + k < C) ? raw_bits<TIn>(src[size_t(k) * HW]) : 0u;
-      uint4 q;
-      if constexpr (G == 4) {
-        q = make_uint4(bits[0], bits[1], bits[2], bits[3]);
-      } else {
-        q = make_uint4(bits[0] | (bits[1] << 16), bits[2] | (bits[3] << 16), bits[4] | (bits[5] << 16),
-                       bits[6] | (bits[7] << 16));
+        for (int u = 0; u < NV; ++u)
+          if (u < N && rpass[u] == pass && idx >= rbase[u]) v = u;
+        const int li = idx - rbase[v];
+        const int py = int((float(li) + 0.5f) * rinv[v]);
+        const int px = li - py * rbw[v];
+        const int gx = rx[v] + px, gy = ry[v] + py;
+        const bool in = (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
+        const TIn* src = fb + (size_t(v) * C + c0) * HW + (in ? size_t(gy) * W + gx : 0);
+        uint32_t bits[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) bits[k] = (in && c0 + k < C) ? raw_bits<TIn>(src[size_t(k) * HW]) : 0u;
+        uint4 q;
+        if constexpr (G == 4) {
+          q = make_uint4(bits[0], bits[1], bits[2], bits[3]);
+        } else {
+          q = make_uint4(bits[0] | (bits[1] << 16), bits[2] | (bits[3] << 16), bits[4] | (bits[5] << 16),
+                         bits[6] | (bits[7] << 16));
+        }
+        stage[idx] = q;
       }
-      stage[idx] = q;
-    }
-    __syncthreads();
+      __syncthreads();
 
-    // ---- sample, aggregate over views, store: one voxel at a time ----------------
-#pragma unroll
-    for (int k = 0; k < VPT; ++k) {
-      float sv[G][NV];
+      // ---- sample this pass's views -----------------------------------------------
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
-        if (v >= N) break;
-        {
+        if (v >= N || rpass[v] != pass) continue;
+#pragma unroll
+        for (int k = 0; k < VPT; ++k) {
           float a[G], bq[G], cq[G], d[G];
           if (has[v][k]) {
             const int o = slot[v][k];
@@ -294,20 +299,25 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
           }
 #pragma unroll
           for (int ch = 0; ch < G; ++ch)
-            sv[ch][v] = __builtin_fmaf(d[ch], w[v][k][3], __builtin_fmaf(cq[ch], w[v][k][2],
-                        __builtin_fmaf(bq[ch], w[v][k][1], a[ch] * w[v][k][0])));
+            sv[k][ch][v] = __builtin_fmaf(d[ch], w[v][k][3], __builtin_fmaf(cq[ch], w[v][k][2],
+                           __builtin_fmaf(bq[ch], w[v][k][1], a[ch] * w[v][k][0])));
         }
       }
+      __syncthreads();                                // stage[] is rewritten next
+    }
+
+    // ---- aggregate over views, store ------------------------------------------------
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
 #pragma unroll
       for (int ch = 0; ch < G; ++ch) {
         const int c = c0 + ch;
         if (c < C) {
-          const float r = aggregate<AGG, NV>(sv[ch], N, cfb ? cfb + c : nullptr, C);
+          const float r = aggregate<AGG, NV>(sv[k][ch], N, cfb ? cfb + c : nullptr, C);
           if (act[k]) store_elem(out + (size_t(b) * C + c) * nvox + vox[k], r);
         }
       }
     }
-    __syncthreads();                                  // stage[] is rewritten by the next group
   }
 }
 
@@ -316,6 +326,10 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
 template <int AGG, typename TIn, typename TOut>
 int launch_tiled(const void* feat, const float* P, const float* coords, const float* conf, void* out, int B,
                  int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, hipStream_t s) {
+  // LDS slot budget per pass; MVN_UNPROJECT_LDS_SLOTS lowers it (tests force the multi-pass
+  // and global-gather paths with it).
+  int budget = kSlots;
+  if (const char* e = getenv("MVN_UNPROJECT_LDS_SLOTS")) budget = max(2, min(kSlots, atoi(e)));
   auto blocks = [&](auto shape) {
     using S = decltype(shape);
     return (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) * ((Vz + S::TZ - 1) / S::TZ);
@@ -325,13 +339,13 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
     if (nb > INT_MAX) return MVN_ERR_SHAPE;
     unproject_tiled<AGG, TIn, TOut, 4><<<int(nb), kThreads, 0, s>>>(
         static_cast<const TIn*>(feat), P, coords, conf, static_cast<TOut*>(out), B, N, C, H, W, Vx, Vy, Vz,
-        align_corners);
+        align_corners, budget);
   } else {
     const long long nb = blocks(TileShape<8>{});
     if (nb > INT_MAX) return MVN_ERR_SHAPE;
     unproject_tiled<AGG, TIn, TOut, 8><<<int(nb), kThreads, 0, s>>>(
         static_cast<const TIn*>(feat), P, coords, conf, static_cast<TOut*>(out), B, N, C, H, W, Vx, Vy, Vz,
-        align_corners);
+        align_corners, budget);
   }
   return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
 }

@@ -52,6 +52,35 @@ def test_unproject_matches_reference_golden(golden, device, method, ac):
     assert_unproject_parity(out.cpu().numpy(), d[f"{method}_ac{ac}"], method)
 
 
+# every code path of the tiled kernel: one LDS pass (default), several passes (small
+# budget), the global-gather fallback (budget below one footprint), and the simple kernel
+KERNEL_PATHS = {
+    "lds_1pass": {},
+    "lds_multipass": {"MVN_UNPROJECT_LDS_SLOTS": "120"},
+    "global_fallback": {"MVN_UNPROJECT_LDS_SLOTS": "3"},
+    "simple": {"MVN_UNPROJECT_KERNEL": "simple"},
+}
+
+
+@pytest.mark.parametrize("path", sorted(KERNEL_PATHS))
+@pytest.mark.parametrize("method", METHODS)
+def test_unproject_every_kernel_path_matches_golden(golden, device, monkeypatch, path, method):
+    for k, v in KERNEL_PATHS[path].items():
+        monkeypatch.setenv(k, v)
+    d = golden("unproject_small.npz")
+    for ac in (0, 1):
+        out = _op().unproject_heatmaps(_t(d["feat"], device), _t(d["proj"], device), _t(d["coords"], device),
+                                       method, _t(d["conf"], device), align_corners=bool(ac))
+        assert_unproject_parity(out.cpu().numpy(), d[f"{method}_ac{ac}"], method)
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(2, n_views=6, channels=10, heatmap=40, volume=16, seed=31)
+    ref = capi.unproject(vb.features.numpy(), vb.proj.numpy(), vb.coords.numpy(), method,
+                         np.ones((2, 6, 10), np.float32))
+    out = _op().unproject_heatmaps(vb.features.to(device), vb.proj.to(device), vb.coords.to(device), method,
+                                   torch.ones((2, 6, 10), device=device))
+    assert_unproject_parity(out.cpu().numpy(), ref, method)
+
+
 @pytest.mark.parametrize("method", ("sum", "softmax"))
 def test_unproject_bf16_matches_reference_golden(golden, device, method):
     d = golden("unproject_small.npz")

@@ -52,32 +52,56 @@ def test_unproject_matches_reference_golden(golden, device, method, ac):
     assert_unproject_parity(out.cpu().numpy(), d[f"{method}_ac{ac}"], method)
 
 
-# every code path of the tiled kernel: one LDS pass (default), several passes (small
-# budget), the global-gather fallback (budget below one footprint), and the simple kernel
-KERNEL_PATHS = {
-    "lds_1pass": {},
-    "lds_multipass": {"MVN_UNPROJECT_LDS_SLOTS": "120"},
-    "global_fallback": {"MVN_UNPROJECT_LDS_SLOTS": "3"},
-    "simple": {"MVN_UNPROJECT_KERNEL": "simple"},
-}
+def tile_footprints(proj, coords, H, W, tile):
+    """Per (frame, tile, view) LDS slots the tiled kernel stages (its bbox rule, in numpy):
+    lets a test pick a budget that forces several passes / the global fallback."""
+    TX, TY, TZ = tile
+    B, Vx, Vy, Vz = coords.shape[:4]
+    P = proj.astype(np.float64)
+    X = np.concatenate([coords, np.ones(coords.shape[:4] + (1,))], -1).astype(np.float64)
+    uvw = np.einsum("bvrk,bxyzk->bvxyzr", P, X)
+    w = np.where(uvw[..., 2] == 0, 1.0, uvw[..., 2])
+    fx = np.floor((2 * (uvw[..., 0] / w / H - 0.5) + 1) * W / 2 - 0.5)
+    fy = np.floor((2 * (uvw[..., 1] / w / W - 0.5) + 1) * H / 2 - 0.5)
+    ok = (fx >= -1) & (fx < W) & (fy >= -1) & (fy < H) & (uvw[..., 2] > 0)
+    out = []
+    for b in range(B):
+        for x in range(0, Vx, TX):
+            for y in range(0, Vy, TY):
+                for z in range(0, Vz, TZ):
+                    areas = []
+                    for v in range(P.shape[1]):
+                        m = ok[b, v, x:x + TX, y:y + TY, z:z + TZ]
+                        a = fx[b, v, x:x + TX, y:y + TY, z:z + TZ][m]
+                        c = fy[b, v, x:x + TX, y:y + TY, z:z + TZ][m]
+                        areas.append(0 if a.size == 0 else int((a.max() - a.min() + 2) * (c.max() - c.min() + 2)))
+                    out.append(areas)
+    return np.array(out)
 
 
-@pytest.mark.parametrize("path", sorted(KERNEL_PATHS))
+@pytest.mark.parametrize("path", ("lds_1pass", "lds_multipass", "global_fallback", "simple"))
 @pytest.mark.parametrize("method", METHODS)
-def test_unproject_every_kernel_path_matches_golden(golden, device, monkeypatch, path, method):
-    for k, v in KERNEL_PATHS[path].items():
-        monkeypatch.setenv(k, v)
-    d = golden("unproject_small.npz")
-    for ac in (0, 1):
-        out = _op().unproject_heatmaps(_t(d["feat"], device), _t(d["proj"], device), _t(d["coords"], device),
-                                       method, _t(d["conf"], device), align_corners=bool(ac))
-        assert_unproject_parity(out.cpu().numpy(), d[f"{method}_ac{ac}"], method)
+def test_unproject_every_kernel_path(device, monkeypatch, path, method):
+    """Each code path of the unprojection — one LDS pass, several LDS passes, the
+    global-gather fallback and the simple kernel — against the oracle."""
     from mvn_rocm import synth
-    vb = synth.volumetric_batch(2, n_views=6, channels=10, heatmap=40, volume=16, seed=31)
-    ref = capi.unproject(vb.features.numpy(), vb.proj.numpy(), vb.coords.numpy(), method,
-                         np.ones((2, 6, 10), np.float32))
+    vb = synth.volumetric_batch(2, n_views=4, channels=10, heatmap=64, volume=32, seed=31)
+    feat, proj, coords = vb.features.numpy(), vb.proj.numpy(), vb.coords.numpy()
+    areas = tile_footprints(proj, coords, 64, 64, (8, 8, 8))
+    if path == "lds_multipass":        # every footprint fits alone, no tile's views fit together
+        budget = int(areas.max()) + 64        # margin: the kernel rounds in f32
+        assert (areas.sum(1) + 1 > budget).any()
+        monkeypatch.setenv("MVN_UNPROJECT_LDS_SLOTS", str(budget))
+    elif path == "global_fallback":    # some single footprints exceed the budget
+        budget = int(np.median(areas[areas > 0]))
+        assert (areas.max(1) > budget - 1).any() and (areas.max(1) <= budget - 1).any()
+        monkeypatch.setenv("MVN_UNPROJECT_LDS_SLOTS", str(budget))
+    elif path == "simple":
+        monkeypatch.setenv("MVN_UNPROJECT_KERNEL", "simple")
+    conf = np.random.default_rng(2).uniform(0, 1, (2, 4, 10)).astype(np.float32)
+    ref = capi.unproject(feat, proj, coords, method, conf)
     out = _op().unproject_heatmaps(vb.features.to(device), vb.proj.to(device), vb.coords.to(device), method,
-                                   torch.ones((2, 6, 10), device=device))
+                                   _t(conf, device))
     assert_unproject_parity(out.cpu().numpy(), ref, method)
 
 

@@ -5,21 +5,26 @@
 //
 // Why: a lane per voxel gathering its 4 taps per (view, channel) straight from the NCHW
 // maps touches a different cache line per lane (neighbouring z-voxels project ~1.6 px
-// apart, i.e. onto different image rows), so the gathers run at L1/L2 request rate, not
-// bandwidth.  Here a block owns a compact voxel tile (TX x TY x TZ).  For every view it
-//   1. projects its voxels once (geometry kept in registers),
-//   2. reduces the bounding box of their bilinear footprints (+1 px each way),
-//   3. stages that footprint for G channels into LDS channels-last — 16 bytes per pixel
-//      (4 f32 / 8 bf16 channels) — reading the NCHW rows coalesced and writing ZERO for
-//      pixels outside the image, which is exactly ATen's padding_mode='zeros',
-//   4. samples: 4 x ds_read_b128 per voxel-view give the 4 taps of G channels.
-// Views are aggregated in registers (max-first softmax: one exp per sample) and each
-// channel plane of the tile is written with z-consecutive lanes.  Blocks are remapped
-// XCD-contiguously so a frame's maps stay in one XCD's L2 and z-neighbouring tiles
-// (which share output lines) run back to back on the same L2.
+// apart, i.e. onto different image rows), so gathers run at L1/L2 request rate, not
+// bandwidth.  Here a block owns a compact 8x8x8 voxel tile.  Once per block it
+//   1. projects its voxels in every view (geometry kept in registers),
+//   2. reduces per view the bounding box of the bilinear footprints (+1 px each way) and
+//      lays the N boxes out in LDS channels-last, 16 bytes per pixel (4 f32 / 8 bf16
+//      channels), with an odd row pitch so that z-neighbouring lanes spread over banks,
+//   3. turns every LDS pixel slot this thread stages into one byte offset into the
+//      frame's NCHW maps (or an out-of-range offset for pixels outside the image).
+// Then per group of G channels staging is only buffer loads — whose hardware range check
+// returns 0 for out-of-range offsets, which is exactly ATen's padding_mode='zeros' — and
+// one ds_write_b128 per pixel, and sampling is 4 ds_read_b128 per voxel-view.  The next
+// group's loads are in flight while the current group is sampled (two LDS buffers, one
+// barrier per group).  Views are aggregated in registers and each channel plane is
+// stored through a buffer descriptor (z-consecutive lanes).  Blocks are remapped
+// XCD-contiguously: a frame's maps stay in one XCD's L2 and z-neighbouring tiles, which
+// share output lines, run back to back there.
 //
-// Footprints that do not fit the LDS budget together are staged in several passes; only a
-// single footprint larger than the whole budget sends its block to direct global gathers.
+// Footprints that do not fit one LDS buffer together are staged in several passes
+// (slower, unpipelined); a single footprint larger than a whole buffer (a camera inside
+// the cuboid) sends its block to direct global gathers.
 #include <stdlib.h>
 
 #include "unproject_common.hpp"
@@ -30,11 +35,38 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
-constexpr int kSlots = 2048;          // 16-byte LDS pixel slots (32 KiB); slot 0 is a zero pad
+constexpr int kBuf = 1536;                        // 16-byte LDS pixel slots per buffer (24 KiB)
+constexpr int kMaxSlotsPerThread = kBuf / kThreads;
+constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any frame
 
-template <int NV> struct TileShape;                 // tile dims and voxels per thread
+template <int NV> struct TileShape;               // tile dims and voxels per thread
 template <> struct TileShape<4> { static constexpr int TX = 8, TY = 8, TZ = 8, VPT = 2; };
 template <> struct TileShape<8> { static constexpr int TX = 4, TY = 8, TZ = 8, VPT = 1; };
+
+// Buffer descriptor from block-uniform inputs, provably in SGPRs (cdna_hip_programming.md T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(a >> 32));
+  void* p = reinterpret_cast<void*>((uint64_t(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, int(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
+}
+
+template <typename T> __device__ __forceinline__ uint32_t buf_load(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
+template <> __device__ __forceinline__ uint32_t buf_load<float>(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, v, s, 0);
+}
+template <> __device__ __forceinline__ uint32_t buf_load<uint16_t>(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+  return __builtin_amdgcn_raw_buffer_load_b16(r, v, s, 0);
+}
+
+template <typename T> __device__ __forceinline__ void buf_store(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
+template <> __device__ __forceinline__ void buf_store<float>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, 0);
+}
+template <> __device__ __forceinline__ void buf_store<uint16_t>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, 0);
+}
 
 // 16-byte slot <-> G floats
 __device__ __forceinline__ void unpack(const uint4& q, float (&v)[4]) {
@@ -48,12 +80,36 @@ __device__ __forceinline__ void unpack(const uint4& q, float (&v)[8]) {
     v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
   }
 }
+template <int G> __device__ __forceinline__ uint4 pack(const uint32_t (&b)[G]) {
+  if constexpr (G == 4) return make_uint4(b[0], b[1], b[2], b[3]);
+  else return make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
+}
 
-template <typename TIn> __device__ __forceinline__ uint32_t raw_bits(TIn v);
-template <> __device__ __forceinline__ uint32_t raw_bits<float>(float v) { return __float_as_uint(v); }
-template <> __device__ __forceinline__ uint32_t raw_bits<uint16_t>(uint16_t v) { return v; }
+// View aggregation, fast form for the staged path.  sum / max / conf are the reference's
+// sequential f32 op order (bit-exact); softmax is max-first with exp2 and one reciprocal.
+template <int AGG, int NV>
+__device__ __forceinline__ float aggregate_fast(const float (&s)[NV], int N, const float* __restrict__ cf, int cstride) {
+  if constexpr (AGG != MVN_AGG_SOFTMAX) {
+    return aggregate<AGG, NV>(s, N, cf, cstride);
+  } else {
+    constexpr float kLog2e = 1.4426950408889634f;
+    float m = s[0];
+#pragma unroll
+    for (int v = 1; v < NV; ++v) if (v < N) m = fmaxf(m, s[v]);
+    const float ml = m * kLog2e;
+    float den = 0.f, num = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      if (v < N) {
+        const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(s[v], kLog2e, -ml));
+        den += e;
+        num = __builtin_fmaf(s[v], e, num);
+      }
+    return num * __builtin_amdgcn_rcpf(den);
+  }
+}
 
-// One voxel, all channels, taps gathered from global memory (LDS-overflow fallback).
+// One voxel, all channels, taps gathered from global memory (oversize-footprint fallback).
 // Rolled loops and geometry recomputed per (channel, view): slow but register-lean, so
 // the staged path's register allocation is unaffected.  Same arithmetic and op order.
 template <int AGG, typename TIn, typename TOut>
@@ -100,14 +156,14 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ, VPT = S::VPT;
   static_assert(TX * TY * TZ == kThreads * VPT, "tile must give every thread VPT voxels");
   constexpr int G = 16 / int(sizeof(TIn));            // channels per 16-byte slot
+  constexpr int MS = kMaxSlotsPerThread;
 
-  __shared__ uint4 stage[kSlots];
+  __shared__ uint4 stage[2 * kBuf];
   __shared__ int red[kWaves][NV][4];
-  __shared__ int region[NV][4];                       // xs, ys, bw, first slot (-1: global fallback)
-  __shared__ int region_end[NV];
+  __shared__ int region[NV][6];                       // xs, ys, bw, pitch, first slot, end slot
   __shared__ int region_pass[NV];
-  __shared__ float region_inv_bw[NV];
-  __shared__ int block_info[1];                       // number of LDS passes, -1 = global fallback
+  __shared__ float region_inv_pitch[NV];
+  __shared__ int block_info[2];                       // passes (-1: global fallback), slots of pass 0
 
   // ---- which tile (XCD-contiguous order, z-tiles fastest) -------------------------
   const int nTx = (Vx + TX - 1) / TX, nTy = (Vy + TY - 1) / TY, nTz = (Vz + TZ - 1) / TZ;
@@ -121,10 +177,10 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int lz = t % TZ, ly = (t / TZ) % TY, lx = t / (TZ * TY);
   const int nvox = Vx * Vy * Vz;
-  const size_t HW = size_t(H) * W;
+  const int HW = H * W;
   const float* Pb = P + size_t(b) * N * 12;
-
-  if (t == 0) stage[0] = make_uint4(0, 0, 0, 0);
+  const TIn* fb = feat + size_t(b) * N * C * HW;
+  const float* cfb = conf ? conf + size_t(b) * N * C : nullptr;
 
   // ---- voxels of this thread ------------------------------------------------------
   int vox[VPT];
@@ -185,10 +241,7 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
   }
   __syncthreads();
   if (t == 0) {
-    // Pack the views' footprints into LDS passes (first fit in view order).  Normally all
-    // N views fit one pass; a close camera needs more passes, never a slow path.  Only a
-    // single footprint larger than the whole budget sends the block to global gathers.
-    int next = 1, pass = 0;                           // slot 0 stays a zero pad
+    int next = 0, pass = 0, slots0 = 0;
     bool too_big = false;
     for (int v = 0; v < NV; ++v) {
       if (v >= N) break;
@@ -199,39 +252,39 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
       }
       int bw = 0, bh = 0;
       if (x0 <= x1) { bw = x1 - x0 + 2; bh = y1 - y0 + 2; }   // +1 px for the east / south taps
-      const long long area = (long long)bw * bh;
-      if (area > budget - 1) too_big = true;
-      if (next + area > budget) { ++pass; next = 1; }
-      region[v][0] = x0; region[v][1] = y0; region[v][2] = bw; region[v][3] = next;
-      region_end[v] = next + int(area);
+      const int pitch = bw | 1;                                 // odd: spreads rows over banks
+      const long long area = (long long)pitch * bh;
+      if (area > budget) too_big = true;
+      if (next + area > budget) { ++pass; next = 0; }
+      region[v][0] = x0; region[v][1] = y0; region[v][2] = bw; region[v][3] = pitch;
+      region[v][4] = next; region[v][5] = next + int(area);
       region_pass[v] = pass;
-      region_inv_bw[v] = bw > 0 ? 1.f / float(bw) : 0.f;
+      region_inv_pitch[v] = 1.f / float(pitch);
       next += int(area);
+      if (pass == 0) slots0 = next;
     }
     block_info[0] = too_big ? -1 : pass + 1;
+    block_info[1] = slots0;
   }
   __syncthreads();
 
-  int rx[NV], ry[NV], rbw[NV], rbase[NV], rend[NV], rpass[NV];
+  int rx[NV], ry[NV], rbw[NV], rpitch[NV], rbase[NV], rend[NV], rpass[NV];
   float rinv[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {       // block-uniform: keep in SGPRs
     rx[v] = __builtin_amdgcn_readfirstlane(region[v][0]);
     ry[v] = __builtin_amdgcn_readfirstlane(region[v][1]);
     rbw[v] = __builtin_amdgcn_readfirstlane(region[v][2]);
-    rbase[v] = __builtin_amdgcn_readfirstlane(region[v][3]);
-    rend[v] = __builtin_amdgcn_readfirstlane(region_end[v]);
+    rpitch[v] = __builtin_amdgcn_readfirstlane(region[v][3]);
+    rbase[v] = __builtin_amdgcn_readfirstlane(region[v][4]);
+    rend[v] = __builtin_amdgcn_readfirstlane(region[v][5]);
     rpass[v] = __builtin_amdgcn_readfirstlane(region_pass[v]);
-    rinv[v] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(region_inv_bw[v])));
+    rinv[v] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(region_inv_pitch[v])));
   }
   const int npass = __builtin_amdgcn_readfirstlane(block_info[0]);
 
-  const TIn* fb = feat + size_t(b) * N * C * HW;
-  const float* cfb = conf ? conf + size_t(b) * N * C : nullptr;
-
   if (npass < 0) {
-    // Pathological geometry (one view's footprint exceeds the whole LDS budget): the block
-    // gathers straight from global memory instead; same arithmetic and op order.
+    // A single footprint exceeds the LDS buffer: gather straight from global memory.
 #pragma unroll
     for (int k = 0; k < VPT; ++k)
       if (act[k])
@@ -240,84 +293,147 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
     return;
   }
 
-  // slot of each voxel-view's north-west tap
-  int slot[NV][VPT];
+  const __amdgpu_buffer_rsrc_t frs = make_rsrc(fb, uint32_t(size_t(N) * C * HW * sizeof(TIn)));
+  const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + size_t(b) * C * nvox, uint32_t(size_t(C) * nvox * sizeof(TOut)));
+  uint32_t ooff[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) ooff[k] = act[k] ? uint32_t(vox[k]) * uint32_t(sizeof(TOut)) : kOob;
+
+  // LDS byte offsets of each voxel-view's north-west and south-west taps (buffer 0)
+  uint32_t anw[NV][VPT], asw[NV][VPT];
 #pragma unroll
   for (int v = 0; v < NV; ++v)
 #pragma unroll
-    for (int k = 0; k < VPT; ++k)
-      slot[v][k] = rbase[v] + (fy[v][k] - ry[v]) * rbw[v] + (fx[v][k] - rx[v]);
+    for (int k = 0; k < VPT; ++k) {
+      const int slot = rbase[v] + (fy[v][k] - ry[v]) * rpitch[v] + (fx[v][k] - rx[v]);
+      anw[v][k] = uint32_t(slot) * 16u;
+      asw[v][k] = uint32_t(slot + rpitch[v]) * 16u;
+    }
 
+  // sample voxel k's views of `pass` from an LDS buffer into sv[ch][v]
+  auto sample_voxel = [&](const char* buf, int pass, int k, float (&sv)[G][NV]) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (v >= N || rpass[v] != pass) continue;
+      float a[G], bq[G], cq[G], d[G];
+      if (has[v][k]) {
+        unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k]), a);
+        unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k] + 16), bq);
+        unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k]), cq);
+        unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k] + 16), d);
+      } else {
+#pragma unroll
+        for (int ch = 0; ch < G; ++ch) a[ch] = bq[ch] = cq[ch] = d[ch] = 0.f;
+      }
+#pragma unroll
+      for (int ch = 0; ch < G; ++ch)
+        sv[ch][v] = __builtin_fmaf(d[ch], w[v][k][3], __builtin_fmaf(cq[ch], w[v][k][2],
+                    __builtin_fmaf(bq[ch], w[v][k][1], a[ch] * w[v][k][0])));
+    }
+  };
+  auto aggregate_store = [&](int c0, int k, const float (&sv)[G][NV]) {
+#pragma unroll
+    for (int ch = 0; ch < G; ++ch) {
+      const int c = c0 + ch;
+      if (c >= C) break;
+      const uint32_t soff = uint32_t(c) * uint32_t(nvox) * uint32_t(sizeof(TOut));
+      buf_store<TOut>(aggregate_fast<AGG, NV>(sv[ch], N, cfb ? cfb + c : nullptr, C), ors, ooff[k], soff);
+    }
+  };
+
+  if (npass == 1) {
+    // ---- fast path: one pass, staging descriptors in registers, two LDS buffers -----
+    const int total = block_info[1];
+    uint32_t goff[MS];
+#pragma unroll
+    for (int i = 0; i < MS; ++i) {
+      const int idx = t + kThreads * i;
+      int v = 0;
+#pragma unroll
+      for (int u = 1; u < NV; ++u)
+        if (u < N && idx >= rbase[u]) v = u;
+      const int li = idx - rbase[v];
+      const int py = int((float(li) + 0.5f) * rinv[v]);
+      const int px = li - py * rpitch[v];
+      const int gx = rx[v] + px, gy = ry[v] + py;
+      const bool in = (idx < total) & (px < rbw[v]) & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
+      goff[i] = in ? uint32_t((v * C * HW + gy * W + gx) * int(sizeof(TIn))) : kOob;
+    }
+    uint32_t pre[MS][G];
+    auto issue = [&](int c0) {
+#pragma unroll
+      for (int i = 0; i < MS; ++i)
+        if (t + kThreads * i < total)
+#pragma unroll
+          for (int k = 0; k < G; ++k) pre[i][k] = buf_load<TIn>(frs, goff[i], uint32_t((c0 + k) * HW * int(sizeof(TIn))));
+    };
+    auto commit = [&](uint4* buf) {
+#pragma unroll
+      for (int i = 0; i < MS; ++i)
+        if (t + kThreads * i < total) buf[t + kThreads * i] = pack<G>(pre[i]);
+    };
+    auto consume = [&](const uint4* buf, int c0) {
+#pragma unroll
+      for (int k = 0; k < VPT; ++k) {        // one voxel at a time bounds the LDS reads in flight
+        float sv[G][NV];
+        sample_voxel(reinterpret_cast<const char*>(buf), 0, k, sv);
+        aggregate_store(c0, k, sv);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+
+    issue(0);
+    commit(stage);
+    __syncthreads();
+    for (int c0 = 0; c0 < C; c0 += 2 * G) {
+      const bool more1 = c0 + G < C, more2 = c0 + 2 * G < C;
+      if (more1) issue(c0 + G);
+      consume(stage, c0);
+      if (!more1) break;
+      commit(stage + kBuf);
+      __syncthreads();
+      if (more2) issue(c0 + 2 * G);
+      consume(stage + kBuf, c0 + G);
+      if (!more2) break;
+      commit(stage);
+      __syncthreads();
+    }
+    return;
+  }
+
+  // ---- several passes per channel group (close cameras): stage, sample, repeat -------
   for (int c0 = 0; c0 < C; c0 += G) {
     float sv[VPT][G][NV];
     for (int pass = 0; pass < npass; ++pass) {
-      // ---- stage this pass's footprints for channels [c0, c0 + G) -----------------
-      int total = 1;
+      int total = 0;
 #pragma unroll
       for (int v = 0; v < NV; ++v) if (v < N && rpass[v] == pass) total = max(total, rend[v]);
-      for (int idx = 1 + t; idx < total; idx += kThreads) {
+      for (int idx = t; idx < total; idx += kThreads) {
         int v = 0;
 #pragma unroll
         for (int u = 0; u < NV; ++u)
           if (u < N && rpass[u] == pass && idx >= rbase[u]) v = u;
         const int li = idx - rbase[v];
         const int py = int((float(li) + 0.5f) * rinv[v]);
-        const int px = li - py * rbw[v];
+        const int px = li - py * rpitch[v];
         const int gx = rx[v] + px, gy = ry[v] + py;
-        const bool in = (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
-        const TIn* src = fb + (size_t(v) * C + c0) * HW + (in ? size_t(gy) * W + gx : 0);
+        const bool in = (px < rbw[v]) & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
+        const uint32_t go = in ? uint32_t((v * C * HW + gy * W + gx) * int(sizeof(TIn))) : kOob;
         uint32_t bits[G];
 #pragma unroll
-        for (int k = 0; k < G; ++k) bits[k] = (in && c0 + k < C) ? raw_bits<TIn>(src[size_t(k) * HW]) : 0u;
-        uint4 q;
-        if constexpr (G == 4) {
-          q = make_uint4(bits[0], bits[1], bits[2], bits[3]);
-        } else {
-          q = make_uint4(bits[0] | (bits[1] << 16), bits[2] | (bits[3] << 16), bits[4] | (bits[5] << 16),
-                         bits[6] | (bits[7] << 16));
-        }
-        stage[idx] = q;
+        for (int k = 0; k < G; ++k) bits[k] = buf_load<TIn>(frs, go, uint32_t((c0 + k) * HW * int(sizeof(TIn))));
+        stage[idx] = pack<G>(bits);
       }
       __syncthreads();
-
-      // ---- sample this pass's views -----------------------------------------------
 #pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        if (v >= N || rpass[v] != pass) continue;
-#pragma unroll
-        for (int k = 0; k < VPT; ++k) {
-          float a[G], bq[G], cq[G], d[G];
-          if (has[v][k]) {
-            const int o = slot[v][k];
-            unpack(stage[o], a);
-            unpack(stage[o + 1], bq);
-            unpack(stage[o + rbw[v]], cq);
-            unpack(stage[o + rbw[v] + 1], d);
-          } else {
-#pragma unroll
-            for (int ch = 0; ch < G; ++ch) a[ch] = bq[ch] = cq[ch] = d[ch] = 0.f;
-          }
-#pragma unroll
-          for (int ch = 0; ch < G; ++ch)
-            sv[k][ch][v] = __builtin_fmaf(d[ch], w[v][k][3], __builtin_fmaf(cq[ch], w[v][k][2],
-                           __builtin_fmaf(bq[ch], w[v][k][1], a[ch] * w[v][k][0])));
-        }
+      for (int k = 0; k < VPT; ++k) {
+        sample_voxel(reinterpret_cast<const char*>(stage), pass, k, sv[k]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __syncthreads();                                // stage[] is rewritten next
+      __syncthreads();
     }
-
-    // ---- aggregate over views, store ------------------------------------------------
 #pragma unroll
-    for (int k = 0; k < VPT; ++k) {
-#pragma unroll
-      for (int ch = 0; ch < G; ++ch) {
-        const int c = c0 + ch;
-        if (c < C) {
-          const float r = aggregate<AGG, NV>(sv[k][ch], N, cfb ? cfb + c : nullptr, C);
-          if (act[k]) store_elem(out + (size_t(b) * C + c) * nvox + vox[k], r);
-        }
-      }
-    }
+    for (int k = 0; k < VPT; ++k) aggregate_store(c0, k, sv[k]);
   }
 }
 
@@ -326,10 +442,14 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
 template <int AGG, typename TIn, typename TOut>
 int launch_tiled(const void* feat, const float* P, const float* coords, const float* conf, void* out, int B,
                  int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, hipStream_t s) {
+  // 32-bit buffer offsets: a frame's maps and volume must stay below 2 GiB
+  if ((long long)N * C * H * W * sizeof(TIn) >= (1LL << 31) ||
+      (long long)C * Vx * Vy * Vz * sizeof(TOut) >= (1LL << 31))
+    return MVN_ERR_SHAPE;
   // LDS slot budget per pass; MVN_UNPROJECT_LDS_SLOTS lowers it (tests force the multi-pass
   // and global-gather paths with it).
-  int budget = kSlots;
-  if (const char* e = getenv("MVN_UNPROJECT_LDS_SLOTS")) budget = max(2, min(kSlots, atoi(e)));
+  int budget = kBuf;
+  if (const char* e = getenv("MVN_UNPROJECT_LDS_SLOTS")) budget = max(1, min(kBuf, atoi(e)));
   auto blocks = [&](auto shape) {
     using S = decltype(shape);
     return (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) * ((Vz + S::TZ - 1) / S::TZ);

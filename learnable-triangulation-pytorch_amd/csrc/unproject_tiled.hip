@@ -27,6 +27,8 @@
 // the cuboid) sends its block to direct global gathers.
 #include <stdlib.h>
 
+#include <utility>
+
 #include "unproject_common.hpp"
 
 namespace mvn {
@@ -38,6 +40,17 @@ constexpr int kWaves = kThreads / kWave;
 constexpr int kBuf = 1536;                        // 16-byte LDS pixel slots per buffer (24 KiB)
 constexpr int kMaxSlotsPerThread = kBuf / kThreads;
 constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any frame
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [0, n).  Keeps per-voxel
+// register arrays statically indexed through the lambdas (no scratch demotion).
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int n, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, n>{});
+}
 
 template <int NV> struct TileShape;               // tile dims and voxels per thread
 template <> struct TileShape<4> { static constexpr int TX = 8, TY = 8, TZ = 8, VPT = 2; };
@@ -107,6 +120,25 @@ __device__ __forceinline__ float aggregate_fast(const float (&s)[NV], int N, con
       }
     return num * __builtin_amdgcn_rcpf(den);
   }
+}
+
+// The LDS region (view) a staged slot index falls in, for one pass.  A select chain over
+// the views: indexing the per-view arrays with a per-lane view number would force them
+// into scratch memory.
+struct SlotRegion {
+  int v, x, y, bw, pitch, base;
+  float inv;
+};
+template <int NV>
+__device__ __forceinline__ SlotRegion find_region(int idx, int pass, int N, const int (&rx)[NV], const int (&ry)[NV],
+                                                  const int (&rbw)[NV], const int (&rpitch)[NV],
+                                                  const int (&rbase)[NV], const int (&rpass)[NV],
+                                                  const float (&rinv)[NV]) {
+  SlotRegion q{0, rx[0], ry[0], rbw[0], rpitch[0], rbase[0], rinv[0]};
+#pragma unroll
+  for (int u = 0; u < NV; ++u)
+    if (u < N && rpass[u] == pass && idx >= rbase[u]) q = SlotRegion{u, rx[u], ry[u], rbw[u], rpitch[u], rbase[u], rinv[u]};
+  return q;
 }
 
 // One voxel, all channels, taps gathered from global memory (oversize-footprint fallback).
@@ -311,7 +343,8 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
     }
 
   // sample voxel k's views of `pass` from an LDS buffer into sv[ch][v]
-  auto sample_voxel = [&](const char* buf, int pass, int k, float (&sv)[G][NV]) {
+  auto sample_voxel = [&](const char* buf, int pass, auto kc, float (&sv)[G][NV]) {
+    constexpr int k = decltype(kc)::value;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (v >= N || rpass[v] != pass) continue;
@@ -331,7 +364,8 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
                     __builtin_fmaf(bq[ch], w[v][k][1], a[ch] * w[v][k][0])));
     }
   };
-  auto aggregate_store = [&](int c0, int k, const float (&sv)[G][NV]) {
+  auto aggregate_store = [&](int c0, auto kc, const float (&sv)[G][NV]) {
+    constexpr int k = decltype(kc)::value;
 #pragma unroll
     for (int ch = 0; ch < G; ++ch) {
       const int c = c0 + ch;
@@ -348,16 +382,13 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
 #pragma unroll
     for (int i = 0; i < MS; ++i) {
       const int idx = t + kThreads * i;
-      int v = 0;
-#pragma unroll
-      for (int u = 1; u < NV; ++u)
-        if (u < N && idx >= rbase[u]) v = u;
-      const int li = idx - rbase[v];
-      const int py = int((float(li) + 0.5f) * rinv[v]);
-      const int px = li - py * rpitch[v];
-      const int gx = rx[v] + px, gy = ry[v] + py;
-      const bool in = (idx < total) & (px < rbw[v]) & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
-      goff[i] = in ? uint32_t((v * C * HW + gy * W + gx) * int(sizeof(TIn))) : kOob;
+      const SlotRegion q = find_region<NV>(idx, 0, N, rx, ry, rbw, rpitch, rbase, rpass, rinv);
+      const int li = idx - q.base;
+      const int py = int((float(li) + 0.5f) * q.inv);
+      const int px = li - py * q.pitch;
+      const int gx = q.x + px, gy = q.y + py;
+      const bool in = (idx < total) & (px < q.bw) & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
+      goff[i] = in ? uint32_t((q.v * C * HW + gy * W + gx) * int(sizeof(TIn))) : kOob;
     }
     uint32_t pre[MS][G];
     auto issue = [&](int c0) {
@@ -373,13 +404,12 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
         if (t + kThreads * i < total) buf[t + kThreads * i] = pack<G>(pre[i]);
     };
     auto consume = [&](const uint4* buf, int c0) {
-#pragma unroll
-      for (int k = 0; k < VPT; ++k) {        // one voxel at a time bounds the LDS reads in flight
+      static_for<VPT>([&](auto kc) {         // one voxel at a time bounds the LDS reads in flight
         float sv[G][NV];
-        sample_voxel(reinterpret_cast<const char*>(buf), 0, k, sv);
-        aggregate_store(c0, k, sv);
+        sample_voxel(reinterpret_cast<const char*>(buf), 0, kc, sv);
+        aggregate_store(c0, kc, sv);
         __builtin_amdgcn_sched_barrier(0);
-      }
+      });
     };
 
     issue(0);
@@ -409,31 +439,26 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
 #pragma unroll
       for (int v = 0; v < NV; ++v) if (v < N && rpass[v] == pass) total = max(total, rend[v]);
       for (int idx = t; idx < total; idx += kThreads) {
-        int v = 0;
-#pragma unroll
-        for (int u = 0; u < NV; ++u)
-          if (u < N && rpass[u] == pass && idx >= rbase[u]) v = u;
-        const int li = idx - rbase[v];
-        const int py = int((float(li) + 0.5f) * rinv[v]);
-        const int px = li - py * rpitch[v];
-        const int gx = rx[v] + px, gy = ry[v] + py;
-        const bool in = (px < rbw[v]) & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
-        const uint32_t go = in ? uint32_t((v * C * HW + gy * W + gx) * int(sizeof(TIn))) : kOob;
+        const SlotRegion q = find_region<NV>(idx, pass, N, rx, ry, rbw, rpitch, rbase, rpass, rinv);
+        const int li = idx - q.base;
+        const int py = int((float(li) + 0.5f) * q.inv);
+        const int px = li - py * q.pitch;
+        const int gx = q.x + px, gy = q.y + py;
+        const bool in = (px < q.bw) & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
+        const uint32_t go = in ? uint32_t((q.v * C * HW + gy * W + gx) * int(sizeof(TIn))) : kOob;
         uint32_t bits[G];
 #pragma unroll
         for (int k = 0; k < G; ++k) bits[k] = buf_load<TIn>(frs, go, uint32_t((c0 + k) * HW * int(sizeof(TIn))));
         stage[idx] = pack<G>(bits);
       }
       __syncthreads();
-#pragma unroll
-      for (int k = 0; k < VPT; ++k) {
-        sample_voxel(reinterpret_cast<const char*>(stage), pass, k, sv[k]);
+      static_for<VPT>([&](auto kc) {
+        sample_voxel(reinterpret_cast<const char*>(stage), pass, kc, sv[decltype(kc)::value]);
         __builtin_amdgcn_sched_barrier(0);
-      }
+      });
       __syncthreads();
     }
-#pragma unroll
-    for (int k = 0; k < VPT; ++k) aggregate_store(c0, k, sv[k]);
+    static_for<VPT>([&](auto kc) { aggregate_store(c0, kc, sv[decltype(kc)::value]); });
   }
 }
 

@@ -6,10 +6,9 @@
 // The caller's `volumes * volume_multiplier` (triangulation.py:353) is fused.
 //
 // Two stream-ordered launches, both HBM-streaming:
-//   pass 1  softargmax_partials : one block per (4096-voxel chunk, frame).  The chunk's
-//           coordinates are loaded ONCE into registers and reused by all J joints; per
-//           joint the block reduces (max, sum e, sum e*x, sum e*y, sum e*z) with wave
-//           shuffles and writes one 5-float partial.
+//   pass 1  softargmax_partials : one wave per (2048-voxel chunk, joint, frame) streams
+//           the chunk once and reduces (max, sum e, sum e*x, sum e*y, sum e*z) with wave
+//           shuffles into one 5-float partial; no barriers, no LDS.
 //   pass 2  softargmax_finalize : one block per (chunk, joint, frame).  Each wave folds
 //           the frame/joint's partials (online-softmax rescale), chunk 0 writes the
 //           coordinates, and every block writes its chunk of the normalised volume.
@@ -22,6 +21,7 @@ constexpr int kSaBlock = 256;
 constexpr int kSaVpt = 16;                      // voxels per thread
 constexpr int kSaChunk = kSaBlock * kSaVpt;     // 4096 voxels per block
 constexpr int kPartial = 5;                     // m, s, sx, sy, sz
+constexpr int kPartChunk = 2048;                // voxels per pass-1 wave
 
 template <typename T> struct Vec;
 template <> struct Vec<float> { static constexpr int n = 4; };
@@ -94,85 +94,74 @@ __device__ __forceinline__ void wave_merge(float& m, float& s, float& sx, float&
   }
 }
 
+// Pass 1: one WAVE per (frame, joint, 2048-voxel chunk) — no barriers, no LDS.  Each lane
+// streams 32 voxels as vector runs, keeps an online (max, sum e, sum e*xyz) and the wave
+// merges the lanes once.  Coordinates are re-read per joint from L2 (they are 12 B per
+// voxel against 2-4 B of volume; L2 absorbs the re-reads, HBM sees them once).
 template <typename T, bool SOFTMAX>
 __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     const T* __restrict__ vol, long long bstride, long long jstride, const float* __restrict__ coords,
     float mult, float* __restrict__ part, int J, int nvox, int nchunk, bool vec_ok) {
   constexpr int VEC = Vec<T>::n;
-  constexpr int RUNS = kSaVpt / VEC;
-  const int b = blockIdx.y, chunk = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  __shared__ float red[2][kSaBlock / kWave][kPartial];
-
-  // this thread's voxels: RUNS runs of VEC consecutive voxels
-  float cx[kSaVpt], cy[kSaVpt], cz[kSaVpt];
+  constexpr int RUNS = kPartChunk / (kWave * VEC);
+  const int chunk = blockIdx.x, b = blockIdx.z;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int j = blockIdx.y * (kSaBlock / kWave) + wid;
+  if (j >= J) return;                                  // whole wave; this kernel has no barriers
+  const T* vj = vol + b * bstride + j * jstride;
   const float* cb = coords + size_t(b) * nvox * 3;
+
+  float m = SOFTMAX ? -INFINITY : 0.f, s = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
 #pragma unroll
   for (int r = 0; r < RUNS; ++r) {
-    const int i0 = chunk * kSaChunk + r * kSaBlock * VEC + tid * VEC;
+    const int i = chunk * kPartChunk + r * kWave * VEC + lane * VEC;
+    float x[VEC];
+    load_run<T, VEC>(vj, i, nvox, vec_ok, x, SOFTMAX ? -INFINITY : 0.f);
+    float c[3 * VEC];
+    if (vec_ok && i + VEC <= nvox) {
+      const float4* cp = reinterpret_cast<const float4*>(cb + size_t(i) * 3);
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      const int i = i0 + k;
-      const bool in = i < nvox;
-      cx[r * VEC + k] = in ? cb[size_t(i) * 3 + 0] : 0.f;
-      cy[r * VEC + k] = in ? cb[size_t(i) * 3 + 1] : 0.f;
-      cz[r * VEC + k] = in ? cb[size_t(i) * 3 + 2] : 0.f;
+      for (int q = 0; q < 3 * VEC / 4; ++q) {
+        const float4 f = cp[q];
+        c[4 * q] = f.x; c[4 * q + 1] = f.y; c[4 * q + 2] = f.z; c[4 * q + 3] = f.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 3 * VEC; ++q) c[q] = (i + q / 3 < nvox) ? cb[size_t(i) * 3 + q] : 0.f;
     }
-  }
-
-  const float fill = SOFTMAX ? -INFINITY : 0.f;
-  for (int j = 0; j < J; ++j) {
-    const T* vj = vol + b * bstride + j * jstride;
-    float x[kSaVpt];
-#pragma unroll
-    for (int r = 0; r < RUNS; ++r) {
-      float t[VEC];
-      load_run<T, VEC>(vj, chunk * kSaChunk + r * kSaBlock * VEC + tid * VEC, nvox, vec_ok, t, fill);
-#pragma unroll
-      for (int k = 0; k < VEC; ++k) x[r * VEC + k] = t[k];
-    }
-    float m = 0.f, s = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
     if constexpr (SOFTMAX) {
-      m = -INFINITY;
+      float mr = -INFINITY;
 #pragma unroll
-      for (int k = 0; k < kSaVpt; ++k) { x[k] = x[k] * mult; m = fmaxf(m, x[k]); }
-      if (m != -INFINITY) {
+      for (int k = 0; k < VEC; ++k) { x[k] = x[k] * mult; mr = fmaxf(mr, x[k]); }
+      const float mn = fmaxf(m, mr);
+      if (mn != -INFINITY) {
+        const float kk = (m == -INFINITY) ? 0.f : __expf(m - mn);
+        s *= kk; sx *= kk; sy *= kk; sz *= kk;
+        m = mn;
 #pragma unroll
-        for (int k = 0; k < kSaVpt; ++k) {
-          const float e = __expf(x[k] - m);
+        for (int k = 0; k < VEC; ++k) {
+          const float e = __expf(x[k] - mn);
           s += e;
-          sx = __builtin_fmaf(e, cx[k], sx);
-          sy = __builtin_fmaf(e, cy[k], sy);
-          sz = __builtin_fmaf(e, cz[k], sz);
+          sx = __builtin_fmaf(e, c[3 * k], sx);
+          sy = __builtin_fmaf(e, c[3 * k + 1], sy);
+          sz = __builtin_fmaf(e, c[3 * k + 2], sz);
         }
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < kSaVpt; ++k) {
+      for (int k = 0; k < VEC; ++k) {
         const float e = fmaxf(x[k] * mult, 0.f);
         s += e;
-        sx = __builtin_fmaf(e, cx[k], sx);
-        sy = __builtin_fmaf(e, cy[k], sy);
-        sz = __builtin_fmaf(e, cz[k], sz);
+        sx = __builtin_fmaf(e, c[3 * k], sx);
+        sy = __builtin_fmaf(e, c[3 * k + 1], sy);
+        sz = __builtin_fmaf(e, c[3 * k + 2], sz);
       }
     }
-    wave_merge<SOFTMAX>(m, s, sx, sy, sz);
-    if (lane == 0) {
-      float* rr = red[j & 1][wid];
-      rr[0] = m; rr[1] = s; rr[2] = sx; rr[3] = sy; rr[4] = sz;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      const float* r0 = red[j & 1][0];
-      float M = r0[0], S = r0[1], X = r0[2], Y = r0[3], Z = r0[4];
-#pragma unroll
-      for (int w = 1; w < kSaBlock / kWave; ++w) {
-        const float* rw = red[j & 1][w];
-        merge<SOFTMAX>(M, S, X, Y, Z, rw[0], rw[1], rw[2], rw[3], rw[4]);
-      }
-      float* o = part + ((size_t(b) * J + j) * nchunk + chunk) * kPartial;
-      o[0] = M; o[1] = S; o[2] = X; o[3] = Y; o[4] = Z;
-    }
+  }
+  wave_merge<SOFTMAX>(m, s, sx, sy, sz);
+  if (lane == 0) {
+    float* o = part + ((size_t(b) * J + j) * nchunk + chunk) * kPartial;
+    o[0] = m; o[1] = s; o[2] = sx; o[3] = sy; o[4] = sz;
   }
 }
 
@@ -180,16 +169,16 @@ template <typename T, typename TO, bool SOFTMAX>
 __global__ __launch_bounds__(kSaBlock) void softargmax_finalize(
     const T* __restrict__ vol, long long bstride, long long jstride, float mult,
     const float* __restrict__ part, float* __restrict__ xyz, TO* __restrict__ out, int J, int nvox,
-    int nchunk, bool vec_ok) {
+    int nchunk, int npart, bool vec_ok) {
   constexpr int VEC = Vec<T>::n;
   constexpr int RUNS = kSaVpt / VEC;
   const int chunk = blockIdx.x, j = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
 
   // every wave folds the (b, j) partials redundantly: no LDS, no barrier
-  const float* pj = part + (size_t(b) * J + j) * nchunk * kPartial;
+  const float* pj = part + (size_t(b) * J + j) * npart * kPartial;
   float m = SOFTMAX ? -INFINITY : 0.f, s = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
-  for (int k = lane; k < nchunk; k += kWave) {
+  for (int k = lane; k < npart; k += kWave) {
     const float* q = pj + size_t(k) * kPartial;
     merge<SOFTMAX>(m, s, sx, sy, sz, q[0], q[1], q[2], q[3], q[4]);
   }
@@ -235,15 +224,16 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_finalize(
 template <typename T, typename TO, bool SOFTMAX>
 int launch(const void* vol, long long bs, long long js, const float* coords, float mult, float* xyz,
            void* out, float* part, int B, int J, int nvox, hipStream_t st) {
-  const int nchunk = (nvox + kSaChunk - 1) / kSaChunk;
+  const int nchunk = (nvox + kSaChunk - 1) / kSaChunk;       // pass-2 blocks per (b, j)
+  const int npart = (nvox + kPartChunk - 1) / kPartChunk;     // pass-1 partials per (b, j)
   const bool vec_ok = (reinterpret_cast<uintptr_t>(vol) % 16 == 0) && (bs * sizeof(T)) % 16 == 0 &&
                       (js * sizeof(T)) % 16 == 0 && (nvox % 8 == 0) &&
                       (out == nullptr || reinterpret_cast<uintptr_t>(out) % 16 == 0);
-  softargmax_partials<T, SOFTMAX><<<dim3(nchunk, B), kSaBlock, 0, st>>>(
-      static_cast<const T*>(vol), bs, js, coords, mult, part, J, nvox, nchunk, vec_ok);
+  softargmax_partials<T, SOFTMAX><<<dim3(npart, (J + kSaBlock / kWave - 1) / (kSaBlock / kWave), B), kSaBlock, 0, st>>>(
+      static_cast<const T*>(vol), bs, js, coords, mult, part, J, nvox, npart, vec_ok);
   if (!launch_ok()) return MVN_ERR_LAUNCH;
   softargmax_finalize<T, TO, SOFTMAX><<<dim3(out ? nchunk : 1, J, B), kSaBlock, 0, st>>>(
-      static_cast<const T*>(vol), bs, js, mult, part, xyz, static_cast<TO*>(out), J, nvox, nchunk, vec_ok);
+      static_cast<const T*>(vol), bs, js, mult, part, xyz, static_cast<TO*>(out), J, nvox, nchunk, npart, vec_ok);
   return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
 }
 
@@ -260,8 +250,8 @@ int launch_mode(int softmax, const void* vol, long long bs, long long js, const 
 extern "C" size_t mvn_softargmax3d_workspace_bytes(int B, int J, int Vx, int Vy, int Vz) {
   if (B <= 0 || J <= 0 || Vx <= 0 || Vy <= 0 || Vz <= 0) return 0;
   const long long nvox = (long long)Vx * Vy * Vz;
-  const long long nchunk = (nvox + mvn::kSaChunk - 1) / mvn::kSaChunk;
-  return size_t(B) * J * nchunk * mvn::kPartial * sizeof(float);
+  const long long npart = (nvox + mvn::kPartChunk - 1) / mvn::kPartChunk;
+  return size_t(B) * J * npart * mvn::kPartial * sizeof(float);
 }
 
 extern "C" int mvn_softargmax3d(const void* vol, int vol_dtype, int64_t vol_bstride, int64_t vol_jstride,

@@ -38,6 +38,8 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
 constexpr int kBuf = 1536;                        // 16-byte LDS pixel slots per buffer (24 KiB)
+constexpr int kZeroSlot = kBuf - 2;               // 2 zero slots ending each buffer: the taps of
+                                                  // voxel-views that sample nothing point there
 constexpr int kMaxSlotsPerThread = kBuf / kThreads;
 constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any frame
 
@@ -179,11 +181,14 @@ __device__ __forceinline__ void gather_voxel(const TIn* __restrict__ fb, const f
   }
 }
 
-template <int AGG, typename TIn, typename TOut, int NV>
-__global__ __launch_bounds__(kThreads) void unproject_tiled(
+// NV = views held in registers (4 or 8); EXACT: the launch has exactly NV views, so every
+// per-view guard is a compile-time constant (no selects in the sampling / aggregation).
+template <int AGG, typename TIn, typename TOut, int NV, bool EXACT>
+__global__ __launch_bounds__(kThreads, (sizeof(TIn) == 4 && NV == 4) ? 3 : 2) void unproject_tiled(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
-    const float* __restrict__ conf, TOut* __restrict__ out, int B, int N, int C, int H, int W, int Vx,
+    const float* __restrict__ conf, TOut* __restrict__ out, int B, int n_views, int C, int H, int W, int Vx,
     int Vy, int Vz, int align_corners, int budget) {
+  const int N = EXACT ? NV : n_views;
   using S = TileShape<NV>;
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ, VPT = S::VPT;
   static_assert(TX * TY * TZ == kThreads * VPT, "tile must give every thread VPT voxels");
@@ -213,6 +218,8 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
   const float* Pb = P + size_t(b) * N * 12;
   const TIn* fb = feat + size_t(b) * N * C * HW;
   const float* cfb = conf ? conf + size_t(b) * N * C : nullptr;
+
+  if (t < 4) stage[(t >> 1) * kBuf + kZeroSlot + (t & 1)] = make_uint4(0, 0, 0, 0);
 
   // ---- voxels of this thread ------------------------------------------------------
   int vox[VPT];
@@ -338,8 +345,8 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
       const int slot = rbase[v] + (fy[v][k] - ry[v]) * rpitch[v] + (fx[v][k] - rx[v]);
-      anw[v][k] = uint32_t(slot) * 16u;
-      asw[v][k] = uint32_t(slot + rpitch[v]) * 16u;
+      anw[v][k] = uint32_t(has[v][k] ? slot : kZeroSlot) * 16u;
+      asw[v][k] = uint32_t(has[v][k] ? slot + rpitch[v] : kZeroSlot) * 16u;
     }
 
   // sample voxel k's views of `pass` from an LDS buffer into sv[ch][v]
@@ -348,16 +355,12 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (v >= N || rpass[v] != pass) continue;
+      // branch-free: voxel-views that sample nothing read the zero slots with zero weights
       float a[G], bq[G], cq[G], d[G];
-      if (has[v][k]) {
-        unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k]), a);
-        unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k] + 16), bq);
-        unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k]), cq);
-        unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k] + 16), d);
-      } else {
-#pragma unroll
-        for (int ch = 0; ch < G; ++ch) a[ch] = bq[ch] = cq[ch] = d[ch] = 0.f;
-      }
+      unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k]), a);
+      unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k] + 16), bq);
+      unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k]), cq);
+      unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k] + 16), d);
 #pragma unroll
       for (int ch = 0; ch < G; ++ch)
         sv[ch][v] = __builtin_fmaf(d[ch], w[v][k][3], __builtin_fmaf(cq[ch], w[v][k][2],
@@ -473,25 +476,28 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
     return MVN_ERR_SHAPE;
   // LDS slot budget per pass; MVN_UNPROJECT_LDS_SLOTS lowers it (tests force the multi-pass
   // and global-gather paths with it).
-  int budget = kBuf;
-  if (const char* e = getenv("MVN_UNPROJECT_LDS_SLOTS")) budget = max(1, min(kBuf, atoi(e)));
+  int budget = kZeroSlot;
+  if (const char* e = getenv("MVN_UNPROJECT_LDS_SLOTS")) budget = max(1, atoi(e));
+  budget = min(budget, kZeroSlot);
   auto blocks = [&](auto shape) {
     using S = decltype(shape);
     return (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) * ((Vz + S::TZ - 1) / S::TZ);
   };
-  if (N <= 4) {
-    const long long nb = blocks(TileShape<4>{});
-    if (nb > INT_MAX) return MVN_ERR_SHAPE;
-    unproject_tiled<AGG, TIn, TOut, 4><<<int(nb), kThreads, 0, s>>>(
+  auto go = [&](auto nv, auto exact) {
+    constexpr int NV = decltype(nv)::value;
+    const long long nb = blocks(TileShape<NV>{});
+    if (nb > INT_MAX) return false;
+    unproject_tiled<AGG, TIn, TOut, NV, decltype(exact)::value><<<int(nb), kThreads, 0, s>>>(
         static_cast<const TIn*>(feat), P, coords, conf, static_cast<TOut*>(out), B, N, C, H, W, Vx, Vy, Vz,
         align_corners, budget);
-  } else {
-    const long long nb = blocks(TileShape<8>{});
-    if (nb > INT_MAX) return MVN_ERR_SHAPE;
-    unproject_tiled<AGG, TIn, TOut, 8><<<int(nb), kThreads, 0, s>>>(
-        static_cast<const TIn*>(feat), P, coords, conf, static_cast<TOut*>(out), B, N, C, H, W, Vx, Vy, Vz,
-        align_corners, budget);
-  }
+    return true;
+  };
+  using I4 = std::integral_constant<int, 4>;
+  using I8 = std::integral_constant<int, 8>;
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  const bool ok = N == 4 ? go(I4{}, T_{}) : N < 4 ? go(I4{}, F_{}) : N == 8 ? go(I8{}, T_{}) : go(I8{}, F_{});
+  if (!ok) return MVN_ERR_SHAPE;
   return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
 }
 

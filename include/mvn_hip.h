@@ -116,6 +116,48 @@ int mvn_softargmax3d(const void* vol, int vol_dtype,
 int mvn_dlt(const float* proj, const float* pts, const float* conf, float* out,
             int B, int N, int J, void* stream);
 
+/* ---- backward (autograd) ------------------------------------------------------------
+ * Gradients of the three ops, replacing the ATen autograd the reference relies on
+ * (grid_sampler_2d / softmax / einsum / svd backward).  Same buffer conventions as above.
+ */
+
+/*
+ * d/d(feat) (and d/d(conf) for MVN_AGG_CONF) of mvn_unproject.
+ *   grad_out   (B, C, Vx, Vy, Vz)  grad_out_dtype (f32 | bf16)
+ *   grad_feat  (B, N, C, H, W) f32, ZERO-INITIALISED by the caller (accumulated with atomics)
+ *   grad_conf  (B, N, C) f32 zero-initialised, or NULL (only read for MVN_AGG_CONF)
+ * No gradient w.r.t. proj / coords (the reference builds both from numpy constants,
+ * triangulation.py:272-341).  N <= 8.  Float atomics: last-bit order nondeterminism.
+ */
+int mvn_unproject_backward(const void* feat, int feat_dtype, const float* proj, const float* coords,
+                           const float* conf, const void* grad_out, int grad_out_dtype,
+                           float* grad_feat, float* grad_conf,
+                           int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+                           int agg, int align_corners, void* stream);
+
+/*
+ * d/d(vol) of mvn_softargmax3d (vol as passed to the forward, i.e. before `multiplier`).
+ *   grad_xyz  (B, J, 3) f32 or NULL;  grad_vol (B, J, Vx, Vy, Vz) contiguous or NULL
+ *   grad_in   (B, J, Vx, Vy, Vz) contiguous, dtype == vol_dtype, fully written
+ *   workspace >= mvn_softargmax3d_backward_workspace_bytes(...) when softmax == 1
+ */
+size_t mvn_softargmax3d_backward_workspace_bytes(int B, int J, int Vx, int Vy, int Vz);
+
+int mvn_softargmax3d_backward(const void* vol, int vol_dtype, int64_t vol_bstride, int64_t vol_jstride,
+                              const float* coords, float multiplier, int softmax,
+                              const float* grad_xyz, const void* grad_vol, int grad_vol_dtype,
+                              void* grad_in, int grad_in_dtype,
+                              void* workspace, size_t workspace_bytes,
+                              int B, int J, int Vx, int Vy, int Vz, void* stream);
+
+/*
+ * d/d(pts) and d/d(conf) of mvn_dlt (eigenvector perturbation of A^T A, f64).
+ *   grad_out (B, J, 3) f32;  grad_pts (B, N, J, 2) f32 written;  grad_conf (B, N, J) f32
+ *   written, or NULL (must be NULL when conf is NULL).
+ */
+int mvn_dlt_backward(const float* proj, const float* pts, const float* conf, const float* grad_out,
+                     float* grad_pts, float* grad_conf, int B, int N, int J, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,358 @@
+// Backward of the unprojection (mvn/utils/op.py:99-163) w.r.t. the feature maps (and the
+// view confidences for 'conf*' aggregation), for gfx950.
+//
+// dL/dfeat[b,v,c,y,x] = sum over voxels i and taps t of  g[b,c,i] * dagg/ds_v(c,i) * w_t(i,v)
+// with, per aggregation (s_v = sample of view v, out = aggregated value):
+//   sum       1
+//   conf*     conf[b,v,c]                 (and dL/dconf[b,v,c] = sum_i g * s_v)
+//   max       1 for the first maximal view, else 0
+//   softmax   p_v (1 + s_v - out),  p = softmax_v(s)
+// Invalid (behind-camera) voxels and out-of-image taps carry no gradient, as in ATen's
+// grid_sampler backward followed by the masked assignment.  Gradients w.r.t. the
+// projection matrices and coordinate volumes are not produced (the reference's callers
+// build both from numpy constants: triangulation.py:272-341).
+//
+// Structure mirrors the forward kernel: a block owns a 4x8x8 voxel tile, stages the
+// forward features of its footprint when the aggregation needs samples, accumulates the
+// tile's tap contributions into an LDS copy of the footprint with ds_add_f32, and flushes
+// it with one global float atomic per touched (pixel, channel) — ~10x fewer global atomics
+// than scattering every tap.  Float atomics make the result order-nondeterministic in the
+// last bits (documented in DESIGN.md).
+#include "unproject_common.hpp"
+
+namespace mvn {
+namespace unproj {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / kWave;
+constexpr int kSlots = 1024;                 // 16-byte slots per LDS buffer (two buffers)
+constexpr int kZero = kSlots - 2;            // zero slots for voxel-views that sample nothing
+constexpr int G = 4;                         // channels per slot (f32 accumulation)
+constexpr int TX = 4, TY = 8, TZ = 8;        // one voxel per thread
+
+template <typename T> __device__ __forceinline__ float ldf(const T* p, size_t i) { return to_f32(p[i]); }
+
+template <int AGG, typename TIn, typename TG, int NV>
+__global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
+    const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
+    const float* __restrict__ conf, const TG* __restrict__ gout, float* __restrict__ gfeat,
+    float* __restrict__ gconf, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners) {
+  constexpr bool kNeedSamples = AGG == MVN_AGG_SOFTMAX || AGG == MVN_AGG_MAX || AGG == MVN_AGG_CONF;
+  __shared__ float4 fstage[kSlots];          // forward features (channels-last)
+  __shared__ float4 gacc[kSlots];            // gradient accumulator (channels-last)
+  __shared__ int red[kWaves][NV][4];
+  __shared__ int region[NV][5];              // xs, ys, bw, pitch, base
+  __shared__ float gconf_acc[NV][G];
+  __shared__ int info[2];                    // total slots (or -1: direct global path)
+
+  const int nTx = (Vx + TX - 1) / TX, nTy = (Vy + TY - 1) / TY, nTz = (Vz + TZ - 1) / TZ;
+  int L = xcd_remap(blockIdx.x, B * nTx * nTy * nTz);
+  const int tz = L % nTz; L /= nTz;
+  const int ty = L % nTy; L /= nTy;
+  const int tx = L % nTx;
+  const int b = L / nTx;
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int X = tx * TX + t / (TZ * TY), Y = ty * TY + (t / TZ) % TY, Z = tz * TZ + t % TZ;
+  const bool act = (X < Vx) & (Y < Vy) & (Z < Vz);
+  const int nvox = Vx * Vy * Vz, HW = H * W;
+  const int vox = act ? (X * Vy + Y) * Vz + Z : 0;
+  const float* cp = coords + (size_t(b) * nvox + vox) * 3;
+  const float cx = cp[0], cy = cp[1], cz = cp[2];
+  const float* Pb = P + size_t(b) * N * 12;
+  const TIn* fb = feat + size_t(b) * N * C * HW;
+  float* gfb = gfeat + size_t(b) * N * C * HW;
+
+  if (t < 2) { fstage[kZero + t] = make_float4(0.f, 0.f, 0.f, 0.f); }
+
+  int fx[NV], fy[NV];
+  float w[NV][4];
+  bool has[NV];
+  int bb[NV][4];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    bb[v][0] = INT_MAX; bb[v][1] = INT_MIN; bb[v][2] = INT_MAX; bb[v][3] = INT_MIN;
+    has[v] = false; fx[v] = fy[v] = 0; w[v][0] = w[v][1] = w[v][2] = w[v][3] = 0.f;
+    if (v < N) {
+      const Proj p = project(Pb + v * 12, cx, cy, cz, H, W, align_corners);
+      const float fx0 = floorf(p.ix), fy0 = floorf(p.iy);
+      const bool h = act & !p.invalid & (fx0 >= -1.f) & (fx0 < float(W)) & (fy0 >= -1.f) & (fy0 < float(H));
+      if (h) {
+        const float a = p.ix - fx0, c = p.iy - fy0;
+        w[v][0] = (1.f - c) * (1.f - a); w[v][1] = (1.f - c) * a; w[v][2] = c * (1.f - a); w[v][3] = c * a;
+        fx[v] = int(fx0); fy[v] = int(fy0);
+        bb[v][0] = fx[v]; bb[v][1] = fx[v]; bb[v][2] = fy[v]; bb[v][3] = fy[v];
+      }
+      has[v] = h;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      bb[v][0] = min(bb[v][0], __shfl_xor(bb[v][0], o, kWave));
+      bb[v][1] = max(bb[v][1], __shfl_xor(bb[v][1], o, kWave));
+      bb[v][2] = min(bb[v][2], __shfl_xor(bb[v][2], o, kWave));
+      bb[v][3] = max(bb[v][3], __shfl_xor(bb[v][3], o, kWave));
+    }
+    if (lane == 0) { red[wid][v][0] = bb[v][0]; red[wid][v][1] = bb[v][1]; red[wid][v][2] = bb[v][2]; red[wid][v][3] = bb[v][3]; }
+  }
+  __syncthreads();
+  if (t == 0) {
+    int next = 0;
+    for (int v = 0; v < NV && v < N; ++v) {
+      int x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN;
+      for (int q = 0; q < kWaves; ++q) {
+        x0 = min(x0, red[q][v][0]); x1 = max(x1, red[q][v][1]);
+        y0 = min(y0, red[q][v][2]); y1 = max(y1, red[q][v][3]);
+      }
+      int bw = 0, bh = 0;
+      if (x0 <= x1) { bw = x1 - x0 + 2; bh = y1 - y0 + 2; }
+      const int pitch = bw | 1;
+      region[v][0] = x0; region[v][1] = y0; region[v][2] = bw; region[v][3] = pitch; region[v][4] = next;
+      next += pitch * bh;
+    }
+    info[0] = next <= kZero ? next : -1;
+  }
+  __syncthreads();
+  const int total = __builtin_amdgcn_readfirstlane(info[0]);
+
+  const TG* gb = gout + size_t(b) * C * nvox + vox;
+  if (total < 0) {
+    // footprint larger than the LDS budget: scatter every tap with a global atomic
+    for (int c = 0; c < C; ++c) {
+      float s[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) s[v] = 0.f;
+      Taps tp[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        if (v < N) {
+          tp[v] = view_taps(Pb + v * 12, cx, cy, cz, H, W, align_corners);
+          if constexpr (kNeedSamples) s[v] = sample(fb + (size_t(v) * C + c) * HW, tp[v]);
+        }
+      const float g = act ? ldf(gb, size_t(c) * nvox) : 0.f;
+      float coef[NV];
+      float out = 0.f, den = 0.f, m = s[0];
+      int arg = 0;
+      if constexpr (AGG == MVN_AGG_SOFTMAX) {
+#pragma unroll
+        for (int v = 1; v < NV; ++v) if (v < N) m = fmaxf(m, s[v]);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) if (v < N) { const float e = __expf(s[v] - m); den += e; out = __builtin_fmaf(s[v], e, out); }
+        out /= den;
+      }
+      if constexpr (AGG == MVN_AGG_MAX) {
+#pragma unroll
+        for (int v = 1; v < NV; ++v) if (v < N && s[v] > s[arg]) arg = v;
+      }
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        if (v >= N) { coef[v] = 0.f; continue; }
+        if constexpr (AGG == MVN_AGG_SUM) coef[v] = g;
+        else if constexpr (AGG == MVN_AGG_CONF) coef[v] = g * conf[(size_t(b) * N + v) * C + c];
+        else if constexpr (AGG == MVN_AGG_MAX) coef[v] = v == arg ? g : 0.f;
+        else coef[v] = g * (__expf(s[v] - m) / den) * (1.f + s[v] - out);
+        if (coef[v] != 0.f) {
+          float* pl = gfb + (size_t(v) * C + c) * HW;
+          if (tp[v].w0 != 0.f) atomicAdd(pl + tp[v].o0, coef[v] * tp[v].w0);
+          if (tp[v].w1 != 0.f) atomicAdd(pl + tp[v].o1, coef[v] * tp[v].w1);
+          if (tp[v].w2 != 0.f) atomicAdd(pl + tp[v].o2, coef[v] * tp[v].w2);
+          if (tp[v].w3 != 0.f) atomicAdd(pl + tp[v].o3, coef[v] * tp[v].w3);
+        }
+        if constexpr (AGG == MVN_AGG_CONF)
+          if (gconf && v < N && g * s[v] != 0.f) atomicAdd(gconf + (size_t(b) * N + v) * C + c, g * s[v]);
+      }
+    }
+    return;
+  }
+
+  int rx[NV], ry[NV], rbw[NV], rpitch[NV], rbase[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    rx[v] = __builtin_amdgcn_readfirstlane(region[v][0]);
+    ry[v] = __builtin_amdgcn_readfirstlane(region[v][1]);
+    rbw[v] = __builtin_amdgcn_readfirstlane(region[v][2]);
+    rpitch[v] = __builtin_amdgcn_readfirstlane(region[v][3]);
+    rbase[v] = __builtin_amdgcn_readfirstlane(region[v][4]);
+  }
+  int slot[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) slot[v] = has[v] ? rbase[v] + (fy[v] - ry[v]) * rpitch[v] + (fx[v] - rx[v]) : kZero;
+
+  for (int c0 = 0; c0 < C; c0 += G) {
+    // ---- zero the accumulator, stage forward features ---------------------------------
+    for (int idx = t; idx < total; idx += kThreads) {
+      gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (kNeedSamples) {
+        int v = 0;
+#pragma unroll
+        for (int u = 1; u < NV; ++u) if (u < N && idx >= rbase[u]) v = u;
+        int px = 0, py = 0, bwv = 0, pv = 1, xs = 0, ys = 0, base = 0;
+#pragma unroll
+        for (int u = 0; u < NV; ++u) if (u == v) { pv = rpitch[u]; bwv = rbw[u]; xs = rx[u]; ys = ry[u]; base = rbase[u]; }
+        py = (idx - base) / pv;
+        px = idx - base - py * pv;
+        const int gx = xs + px, gy = ys + py;
+        const bool in = (px < bwv) & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
+        float q[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) q[k] = (in && c0 + k < C) ? ldf(fb, (size_t(v) * C + c0 + k) * HW + size_t(gy) * W + gx) : 0.f;
+        fstage[idx] = make_float4(q[0], q[1], q[2], q[3]);
+      }
+    }
+    if (t < NV * G) gconf_acc[t / G][t % G] = 0.f;
+    __syncthreads();
+
+    // ---- per voxel: samples, upstream gradient, d agg / d s_v, LDS scatter ------------
+    float g[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) g[k] = (act && c0 + k < C) ? ldf(gb, size_t(c0 + k) * nvox) : 0.f;
+    float s[NV][G];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+#pragma unroll
+      for (int k = 0; k < G; ++k) s[v][k] = 0.f;
+      if constexpr (kNeedSamples) {
+        if (v < N) {
+          const int o = slot[v], o2 = has[v] ? slot[v] + rpitch[v] : kZero;
+          const float4 a = fstage[o], bq = fstage[o + 1], c = fstage[o2], d = fstage[o2 + 1];
+          const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {bq.x, bq.y, bq.z, bq.w};
+          const float cv[4] = {c.x, c.y, c.z, c.w}, dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+          for (int k = 0; k < G; ++k)
+            s[v][k] = __builtin_fmaf(dv[k], w[v][3], __builtin_fmaf(cv[k], w[v][2], __builtin_fmaf(bv[k], w[v][1], av[k] * w[v][0])));
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int c = c0 + k;
+      float coef[NV];
+      if constexpr (AGG == MVN_AGG_SOFTMAX) {
+        float m = s[0][k];
+#pragma unroll
+        for (int v = 1; v < NV; ++v) if (v < N) m = fmaxf(m, s[v][k]);
+        float den = 0.f, out = 0.f, e[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) { e[v] = v < N ? __expf(s[v][k] - m) : 0.f; den += e[v]; out = __builtin_fmaf(s[v][k], e[v], out); }
+        const float inv = 1.f / den;
+        out *= inv;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) coef[v] = g[k] * e[v] * inv * (1.f + s[v][k] - out);
+      } else if constexpr (AGG == MVN_AGG_MAX) {
+        int arg = 0;
+#pragma unroll
+        for (int v = 1; v < NV; ++v) if (v < N && s[v][k] > s[arg][k]) arg = v;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) coef[v] = v == arg ? g[k] : 0.f;
+      } else if constexpr (AGG == MVN_AGG_CONF) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) coef[v] = (v < N && c < C) ? g[k] * conf[(size_t(b) * N + v) * C + c] : 0.f;
+      } else {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) coef[v] = g[k];
+      }
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        if (v >= N || !has[v] || coef[v] == 0.f) continue;
+        float* base0 = reinterpret_cast<float*>(&gacc[slot[v]]) + k;
+        float* base1 = reinterpret_cast<float*>(&gacc[slot[v] + rpitch[v]]) + k;
+        atomicAdd(base0, coef[v] * w[v][0]);
+        atomicAdd(base0 + 4, coef[v] * w[v][1]);
+        atomicAdd(base1, coef[v] * w[v][2]);
+        atomicAdd(base1 + 4, coef[v] * w[v][3]);
+      }
+      if constexpr (AGG == MVN_AGG_CONF) {
+        if (gconf) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            if (v >= N) continue;
+            float part = g[k] * s[v][k];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
+            if (lane == 0 && part != 0.f) atomicAdd(&gconf_acc[v][k], part);
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- flush the footprint: one global atomic per touched (pixel, channel) ---------
+    for (int idx = t; idx < total; idx += kThreads) {
+      int v = 0;
+#pragma unroll
+      for (int u = 1; u < NV; ++u) if (u < N && idx >= rbase[u]) v = u;
+      int bwv = 0, pv = 1, xs = 0, ys = 0, base = 0;
+#pragma unroll
+      for (int u = 0; u < NV; ++u) if (u == v) { pv = rpitch[u]; bwv = rbw[u]; xs = rx[u]; ys = ry[u]; base = rbase[u]; }
+      const int py = (idx - base) / pv, px = idx - base - py * pv;
+      const int gx = xs + px, gy = ys + py;
+      if ((px < bwv) & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H)) {
+        const float4 a = gacc[idx];
+        const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+          if (c0 + k < C && av[k] != 0.f) atomicAdd(gfb + (size_t(v) * C + c0 + k) * HW + size_t(gy) * W + gx, av[k]);
+      }
+    }
+    if constexpr (AGG == MVN_AGG_CONF) {
+      if (gconf && t < NV * G) {
+        const int v = t / G, k = t % G;
+        if (v < N && c0 + k < C && gconf_acc[v][k] != 0.f) atomicAdd(gconf + (size_t(b) * N + v) * C + c0 + k, gconf_acc[v][k]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int AGG, typename TIn, typename TG>
+int launch_bwd(const void* feat, const float* P, const float* coords, const float* conf, const void* gout, float* gfeat,
+               float* gconf, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int ac, hipStream_t s) {
+  const long long nb = (long long)B * ((Vx + TX - 1) / TX) * ((Vy + TY - 1) / TY) * ((Vz + TZ - 1) / TZ);
+  if (nb > INT_MAX) return MVN_ERR_SHAPE;
+  if (N <= 4)
+    unproject_bwd_tiled<AGG, TIn, TG, 4><<<int(nb), kThreads, 0, s>>>(static_cast<const TIn*>(feat), P, coords, conf,
+        static_cast<const TG*>(gout), gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac);
+  else if (N <= 8)
+    unproject_bwd_tiled<AGG, TIn, TG, 8><<<int(nb), kThreads, 0, s>>>(static_cast<const TIn*>(feat), P, coords, conf,
+        static_cast<const TG*>(gout), gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac);
+  else
+    return MVN_ERR_SHAPE;
+  return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
+}
+
+template <typename TIn, typename TG>
+int dispatch_bwd(int agg, const void* feat, const float* P, const float* coords, const float* conf, const void* gout,
+                 float* gfeat, float* gconf, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int ac,
+                 hipStream_t s) {
+  switch (agg) {
+    case MVN_AGG_SUM: return launch_bwd<MVN_AGG_SUM, TIn, TG>(feat, P, coords, conf, gout, gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac, s);
+    case MVN_AGG_MAX: return launch_bwd<MVN_AGG_MAX, TIn, TG>(feat, P, coords, conf, gout, gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac, s);
+    case MVN_AGG_SOFTMAX: return launch_bwd<MVN_AGG_SOFTMAX, TIn, TG>(feat, P, coords, conf, gout, gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac, s);
+    case MVN_AGG_CONF: return launch_bwd<MVN_AGG_CONF, TIn, TG>(feat, P, coords, conf, gout, gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac, s);
+  }
+  return MVN_ERR_ARG;
+}
+
+}  // namespace
+}  // namespace unproj
+}  // namespace mvn
+
+extern "C" int mvn_unproject_backward(const void* feat, int feat_dtype, const float* proj, const float* coords,
+                                      const float* conf, const void* grad_out, int grad_out_dtype, float* grad_feat,
+                                      float* grad_conf, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+                                      int agg, int align_corners, void* stream) {
+  using namespace mvn;
+  if (!feat || !proj || !coords || !grad_out || !grad_feat) return MVN_ERR_ARG;
+  if (agg < MVN_AGG_SUM || agg > MVN_AGG_CONF) return MVN_ERR_ARG;
+  if (agg == MVN_AGG_CONF && !conf) return MVN_ERR_ARG;
+  if (align_corners != 0 && align_corners != 1) return MVN_ERR_ARG;
+  if (B <= 0 || N <= 0 || C <= 0 || H <= 0 || W <= 0 || Vx <= 0 || Vy <= 0 || Vz <= 0) return MVN_ERR_SHAPE;
+  if ((long long)Vx * Vy * Vz > (1LL << 30) || (long long)H * W > (1LL << 30) || N > 8) return MVN_ERR_SHAPE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool f16 = feat_dtype == MVN_DTYPE_BF16, g16 = grad_out_dtype == MVN_DTYPE_BF16;
+  if ((feat_dtype != MVN_DTYPE_F32 && !f16) || (grad_out_dtype != MVN_DTYPE_F32 && !g16)) return MVN_ERR_DTYPE;
+  using namespace mvn::unproj;
+  if (!f16 && !g16) return dispatch_bwd<float, float>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+  if (f16 && g16) return dispatch_bwd<uint16_t, uint16_t>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+  if (f16) return dispatch_bwd<uint16_t, float>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+  return dispatch_bwd<float, uint16_t>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+}

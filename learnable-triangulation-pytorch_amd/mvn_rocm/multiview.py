@@ -38,7 +38,7 @@ class DLTFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, proj, pts, conf):
         out = _ops.dlt(proj, pts, conf)
-        ctx.save_for_backward(proj, pts, conf, out)
+        ctx.save_for_backward(proj, pts, conf)
         return out
 
     @staticmethod

@@ -86,12 +86,13 @@ def integrate_tensor_3d_with_coordinates(volumes, coord_volumes, softmax=True, *
 
 
 class UnprojectFunction(torch.autograd.Function):
-    """autograd surface of op.py:99-163 (backward kernels: see mvn_rocm/_backward.py)."""
+    """autograd surface of op.py:99-163; backward: csrc/unproject_bwd.hip (grads w.r.t. the
+    features and, for 'conf*', the confidences)."""
 
     @staticmethod
     def forward(ctx, feat, proj, coords, conf, agg, align_corners, out_dtype):
         out = _ops.unproject(feat, proj, coords, conf, agg, align_corners, out_dtype)
-        ctx.save_for_backward(feat, proj, coords, conf, out)
+        ctx.save_for_backward(feat, proj, coords, conf)
         ctx.cfg = (agg, align_corners)
         return out
 
@@ -102,12 +103,12 @@ class UnprojectFunction(torch.autograd.Function):
 
 
 class SoftArgmaxFunction(torch.autograd.Function):
-    """autograd surface of op.py:84-96."""
+    """autograd surface of op.py:84-96; backward: csrc/backward.hip."""
 
     @staticmethod
     def forward(ctx, vol, coords, softmax, multiplier, return_volume, out_dtype):
         xyz, out = _ops.softargmax3d(vol, coords, softmax, multiplier, return_volume, out_dtype)
-        ctx.save_for_backward(vol, coords, xyz, out)
+        ctx.save_for_backward(vol, coords)
         ctx.cfg = (softmax, multiplier, return_volume)
         return xyz, out
 

@@ -37,10 +37,9 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
-constexpr int kBuf = 1536;                        // 16-byte LDS pixel slots per buffer (24 KiB)
-constexpr int kZeroSlot = kBuf - 2;               // 2 zero slots ending each buffer: the taps of
-                                                  // voxel-views that sample nothing point there
-constexpr int kMaxSlotsPerThread = kBuf / kThreads;
+// 16-byte LDS pixel slots per buffer (two buffers per block); the last 2 slots of each are
+// zero: the taps of voxel-views that sample nothing point there.
+template <int NV> struct Buf { static constexpr int slots = NV == 4 ? 1024 : 2048; };
 constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any frame
 
 // Compile-time loop: f(std::integral_constant<int, i>) for i in [0, n).  Keeps per-voxel
@@ -55,7 +54,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 template <int NV> struct TileShape;               // tile dims and voxels per thread
-template <> struct TileShape<4> { static constexpr int TX = 8, TY = 8, TZ = 8, VPT = 2; };
+template <> struct TileShape<4> { static constexpr int TX = 4, TY = 8, TZ = 8, VPT = 1; };
 template <> struct TileShape<8> { static constexpr int TX = 4, TY = 8, TZ = 8, VPT = 1; };
 
 // Buffer descriptor from block-uniform inputs, provably in SGPRs (cdna_hip_programming.md T20).
@@ -184,7 +183,7 @@ __device__ __forceinline__ void gather_voxel(const TIn* __restrict__ fb, const f
 // NV = views held in registers (4 or 8); EXACT: the launch has exactly NV views, so every
 // per-view guard is a compile-time constant (no selects in the sampling / aggregation).
 template <int AGG, typename TIn, typename TOut, int NV, bool EXACT>
-__global__ __launch_bounds__(kThreads, (sizeof(TIn) == 4 && NV == 4) ? 3 : 2) void unproject_tiled(
+__global__ __launch_bounds__(kThreads) void unproject_tiled(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ conf, TOut* __restrict__ out, int B, int n_views, int C, int H, int W, int Vx,
     int Vy, int Vz, int align_corners, int budget) {
@@ -193,7 +192,9 @@ __global__ __launch_bounds__(kThreads, (sizeof(TIn) == 4 && NV == 4) ? 3 : 2) vo
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ, VPT = S::VPT;
   static_assert(TX * TY * TZ == kThreads * VPT, "tile must give every thread VPT voxels");
   constexpr int G = 16 / int(sizeof(TIn));            // channels per 16-byte slot
-  constexpr int MS = kMaxSlotsPerThread;
+  constexpr int kBuf = Buf<NV>::slots;
+  constexpr int kZeroSlot = kBuf - 2;
+  constexpr int MS = kBuf / kThreads;                 // staged slots per thread (max)
 
   __shared__ uint4 stage[2 * kBuf];
   __shared__ int red[kWaves][NV][4];
@@ -282,6 +283,7 @@ __global__ __launch_bounds__(kThreads, (sizeof(TIn) == 4 && NV == 4) ? 3 : 2) vo
   if (t == 0) {
     int next = 0, pass = 0, slots0 = 0;
     bool too_big = false;
+    budget = min(budget, kZeroSlot);
     for (int v = 0; v < NV; ++v) {
       if (v >= N) break;
       int x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN;
@@ -474,11 +476,10 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
   if ((long long)N * C * H * W * sizeof(TIn) >= (1LL << 31) ||
       (long long)C * Vx * Vy * Vz * sizeof(TOut) >= (1LL << 31))
     return MVN_ERR_SHAPE;
-  // LDS slot budget per pass; MVN_UNPROJECT_LDS_SLOTS lowers it (tests force the multi-pass
-  // and global-gather paths with it).
-  int budget = kZeroSlot;
+  // LDS slot budget per pass (clamped in-kernel to the buffer); MVN_UNPROJECT_LDS_SLOTS
+  // lowers it (tests force the multi-pass and global-gather paths with it).
+  int budget = 1 << 30;
   if (const char* e = getenv("MVN_UNPROJECT_LDS_SLOTS")) budget = max(1, atoi(e));
-  budget = min(budget, kZeroSlot);
   auto blocks = [&](auto shape) {
     using S = decltype(shape);
     return (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) * ((Vz + S::TZ - 1) / S::TZ);

@@ -5,13 +5,14 @@
 //   V^3 volume of every (b, j), then coords = einsum("bnxyz,bxyzc->bnc") (op.py:94).
 // The caller's `volumes * volume_multiplier` (triangulation.py:353) is fused.
 //
-// Two stream-ordered launches, both HBM-streaming:
+// Three stream-ordered launches (the middle one tiny):
 //   pass 1  softargmax_partials : one wave per (2048-voxel chunk, joint, frame) streams
 //           the chunk once and reduces (max, sum e, sum e*x, sum e*y, sum e*z) with wave
 //           shuffles into one 5-float partial; no barriers, no LDS.
-//   pass 2  softargmax_finalize : one block per (chunk, joint, frame).  Each wave folds
-//           the frame/joint's partials (online-softmax rescale), chunk 0 writes the
-//           coordinates, and every block writes its chunk of the normalised volume.
+//   pass 2  softargmax_combine  : one wave per (frame, joint) folds the partials (online
+//           rescale), writes the coordinates and (max, 1/sum).
+//   pass 3  softargmax_finalize : one block per (4096-voxel chunk, joint, frame) streams
+//           the normalised volume (skipped when the caller does not want it).
 #include "common.hpp"
 
 namespace mvn {
@@ -111,51 +112,61 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
   const T* vj = vol + b * bstride + j * jstride;
   const float* cb = coords + size_t(b) * nvox * 3;
 
+  // Loads are issued for a batch of runs before any arithmetic: the online-max chain
+  // would otherwise expose one memory latency per run.
+  constexpr int BATCH = VEC == 4 ? 4 : 2;            // ~64 loaded floats per batch
   float m = SOFTMAX ? -INFINITY : 0.f, s = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
 #pragma unroll
-  for (int r = 0; r < RUNS; ++r) {
-    const int i = chunk * kPartChunk + r * kWave * VEC + lane * VEC;
-    float x[VEC];
-    load_run<T, VEC>(vj, i, nvox, vec_ok, x, SOFTMAX ? -INFINITY : 0.f);
-    float c[3 * VEC];
-    if (vec_ok && i + VEC <= nvox) {
-      const float4* cp = reinterpret_cast<const float4*>(cb + size_t(i) * 3);
+  for (int r0 = 0; r0 < RUNS; r0 += BATCH) {
+    float x[BATCH][VEC], c[BATCH][3 * VEC];
 #pragma unroll
-      for (int q = 0; q < 3 * VEC / 4; ++q) {
-        const float4 f = cp[q];
-        c[4 * q] = f.x; c[4 * q + 1] = f.y; c[4 * q + 2] = f.z; c[4 * q + 3] = f.w;
+    for (int q = 0; q < BATCH; ++q) {
+      const int i = chunk * kPartChunk + (r0 + q) * kWave * VEC + lane * VEC;
+      load_run<T, VEC>(vj, i, nvox, vec_ok, x[q], SOFTMAX ? -INFINITY : 0.f);
+      if (vec_ok && i + VEC <= nvox) {
+        const float4* cp = reinterpret_cast<const float4*>(cb + size_t(i) * 3);
+#pragma unroll
+        for (int u = 0; u < 3 * VEC / 4; ++u) {
+          const float4 f = cp[u];
+          c[q][4 * u] = f.x; c[q][4 * u + 1] = f.y; c[q][4 * u + 2] = f.z; c[q][4 * u + 3] = f.w;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 3 * VEC; ++u) c[q][u] = (i + u / 3 < nvox) ? cb[size_t(i) * 3 + u] : 0.f;
       }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 3 * VEC; ++q) c[q] = (i + q / 3 < nvox) ? cb[size_t(i) * 3 + q] : 0.f;
     }
     if constexpr (SOFTMAX) {
-      float mr = -INFINITY;
+      float mr = m;
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) { x[k] = x[k] * mult; mr = fmaxf(mr, x[k]); }
-      const float mn = fmaxf(m, mr);
-      if (mn != -INFINITY) {
-        const float kk = (m == -INFINITY) ? 0.f : __expf(m - mn);
+      for (int q = 0; q < BATCH; ++q)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) { x[q][k] = x[q][k] * mult; mr = fmaxf(mr, x[q][k]); }
+      if (mr != -INFINITY) {
+        const float kk = (m == -INFINITY) ? 0.f : __expf(m - mr);
         s *= kk; sx *= kk; sy *= kk; sz *= kk;
-        m = mn;
+        m = mr;
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-          const float e = __expf(x[k] - mn);
-          s += e;
-          sx = __builtin_fmaf(e, c[3 * k], sx);
-          sy = __builtin_fmaf(e, c[3 * k + 1], sy);
-          sz = __builtin_fmaf(e, c[3 * k + 2], sz);
-        }
+        for (int q = 0; q < BATCH; ++q)
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) {
+            const float e = __expf(x[q][k] - mr);
+            s += e;
+            sx = __builtin_fmaf(e, c[q][3 * k], sx);
+            sy = __builtin_fmaf(e, c[q][3 * k + 1], sy);
+            sz = __builtin_fmaf(e, c[q][3 * k + 2], sz);
+          }
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) {
-        const float e = fmaxf(x[k] * mult, 0.f);
-        s += e;
-        sx = __builtin_fmaf(e, c[3 * k], sx);
-        sy = __builtin_fmaf(e, c[3 * k + 1], sy);
-        sz = __builtin_fmaf(e, c[3 * k + 2], sz);
-      }
+      for (int q = 0; q < BATCH; ++q)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          const float e = fmaxf(x[q][k] * mult, 0.f);
+          s += e;
+          sx = __builtin_fmaf(e, c[q][3 * k], sx);
+          sy = __builtin_fmaf(e, c[q][3 * k + 1], sy);
+          sz = __builtin_fmaf(e, c[q][3 * k + 2], sz);
+        }
     }
   }
   wave_merge<SOFTMAX>(m, s, sx, sy, sz);
@@ -165,47 +176,57 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
   }
 }
 
-template <typename T, typename TO, bool SOFTMAX>
-__global__ __launch_bounds__(kSaBlock) void softargmax_finalize(
-    const T* __restrict__ vol, long long bstride, long long jstride, float mult,
-    const float* __restrict__ part, float* __restrict__ xyz, TO* __restrict__ out, int J, int nvox,
-    int nchunk, int npart, bool vec_ok) {
-  constexpr int VEC = Vec<T>::n;
-  constexpr int RUNS = kSaVpt / VEC;
-  const int chunk = blockIdx.x, j = blockIdx.y, b = blockIdx.z;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1);
-
-  // every wave folds the (b, j) partials redundantly: no LDS, no barrier
-  const float* pj = part + (size_t(b) * J + j) * npart * kPartial;
+// Pass 2: one wave per (b, j) folds the pass-1 partials, writes the coordinates and the
+// (max, 1 / sum) the normalisation pass needs.
+template <bool SOFTMAX>
+__global__ __launch_bounds__(kSaBlock) void softargmax_combine(const float* __restrict__ part,
+                                                              float* __restrict__ xyz, float* __restrict__ stat,
+                                                              int BJ, int npart) {
+  const int bj = blockIdx.x * (kSaBlock / kWave) + threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  if (bj >= BJ) return;
+  const float* pj = part + size_t(bj) * npart * kPartial;
   float m = SOFTMAX ? -INFINITY : 0.f, s = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
   for (int k = lane; k < npart; k += kWave) {
     const float* q = pj + size_t(k) * kPartial;
     merge<SOFTMAX>(m, s, sx, sy, sz, q[0], q[1], q[2], q[3], q[4]);
   }
   wave_merge<SOFTMAX>(m, s, sx, sy, sz);
-
-  if (chunk == 0 && tid == 0) {
-    float* o = xyz + (size_t(b) * J + j) * 3;
+  if (lane == 0) {
+    float* o = xyz + size_t(bj) * 3;
     if constexpr (SOFTMAX) {
-      o[0] = sx / s; o[1] = sy / s; o[2] = sz / s;
+      o[0] = sx / s; o[1] = sy / s; o[2] = sz / s;      // op.py:94 on the normalised volume
     } else {
-      o[0] = sx; o[1] = sy; o[2] = sz;
+      o[0] = sx; o[1] = sy; o[2] = sz;                  // relu: no mass normalisation (op.py:91)
     }
+    stat[size_t(bj) * 2] = m;
+    stat[size_t(bj) * 2 + 1] = 1.f / s;
   }
-  if (out == nullptr) return;
+}
 
-  const float inv = 1.f / s;
+// Pass 3: stream the normalised volume, exp(mult * x - max) / sum (or relu(mult * x)).
+template <typename T, typename TO, bool SOFTMAX>
+__global__ __launch_bounds__(kSaBlock) void softargmax_finalize(
+    const T* __restrict__ vol, long long bstride, long long jstride, float mult,
+    const float* __restrict__ stat, TO* __restrict__ out, int J, int nvox, bool vec_ok) {
+  constexpr int VEC = Vec<T>::n;
+  constexpr int RUNS = kSaVpt / VEC;
+  const int chunk = blockIdx.x, j = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x;
+  const float m = stat[(size_t(b) * J + j) * 2], inv = stat[(size_t(b) * J + j) * 2 + 1];
   const T* vj = vol + b * bstride + j * jstride;
   TO* oj = out + (size_t(b) * J + j) * nvox;
+  float t[RUNS][VEC];
+#pragma unroll
+  for (int r = 0; r < RUNS; ++r)
+    load_run<T, VEC>(vj, chunk * kSaChunk + r * kSaBlock * VEC + tid * VEC, nvox, vec_ok, t[r], 0.f);
 #pragma unroll
   for (int r = 0; r < RUNS; ++r) {
     const int i = chunk * kSaChunk + r * kSaBlock * VEC + tid * VEC;
-    float t[VEC];
-    load_run<T, VEC>(vj, i, nvox, vec_ok, t, 0.f);
     float y[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
-      const float v = t[k] * mult;
+      const float v = t[r][k] * mult;
       y[k] = SOFTMAX ? __expf(v - m) * inv : fmaxf(v, 0.f);
     }
     if constexpr (sizeof(TO) == sizeof(T)) {
@@ -232,8 +253,13 @@ int launch(const void* vol, long long bs, long long js, const float* coords, flo
   softargmax_partials<T, SOFTMAX><<<dim3(npart, (J + kSaBlock / kWave - 1) / (kSaBlock / kWave), B), kSaBlock, 0, st>>>(
       static_cast<const T*>(vol), bs, js, coords, mult, part, J, nvox, npart, vec_ok);
   if (!launch_ok()) return MVN_ERR_LAUNCH;
-  softargmax_finalize<T, TO, SOFTMAX><<<dim3(out ? nchunk : 1, J, B), kSaBlock, 0, st>>>(
-      static_cast<const T*>(vol), bs, js, mult, part, xyz, static_cast<TO*>(out), J, nvox, nchunk, npart, vec_ok);
+  float* stat = part + size_t(B) * J * npart * kPartial;
+  softargmax_combine<SOFTMAX><<<(B * J + kSaBlock / kWave - 1) / (kSaBlock / kWave), kSaBlock, 0, st>>>(
+      part, xyz, stat, B * J, npart);
+  if (!launch_ok()) return MVN_ERR_LAUNCH;
+  if (out == nullptr) return MVN_OK;
+  softargmax_finalize<T, TO, SOFTMAX><<<dim3(nchunk, J, B), kSaBlock, 0, st>>>(
+      static_cast<const T*>(vol), bs, js, mult, stat, static_cast<TO*>(out), J, nvox, vec_ok);
   return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
 }
 
@@ -251,7 +277,7 @@ extern "C" size_t mvn_softargmax3d_workspace_bytes(int B, int J, int Vx, int Vy,
   if (B <= 0 || J <= 0 || Vx <= 0 || Vy <= 0 || Vz <= 0) return 0;
   const long long nvox = (long long)Vx * Vy * Vz;
   const long long npart = (nvox + mvn::kPartChunk - 1) / mvn::kPartChunk;
-  return size_t(B) * J * npart * mvn::kPartial * sizeof(float);
+  return size_t(B) * J * (npart * mvn::kPartial + 2) * sizeof(float);   // partials + (max, 1/sum)
 }
 
 extern "C" int mvn_softargmax3d(const void* vol, int vol_dtype, int64_t vol_bstride, int64_t vol_jstride,

@@ -186,7 +186,9 @@ template <int AGG, typename TIn, typename TOut, int NV, bool EXACT>
 __global__ __launch_bounds__(kThreads) void unproject_tiled(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ conf, TOut* __restrict__ out, int B, int n_views, int C, int H, int W, int Vx,
-    int Vy, int Vz, int align_corners, int budget) {
+    int Vy, int Vz, int align_corners, int budget, int ablate) {
+  // ablate (diagnostics only, MVN_UNPROJECT_ABLATE): bit 0 skip the output stores, bit 1
+  // skip the staging loads, bit 2 skip the LDS tap reads (results are wrong; timing only)
   const int N = EXACT ? NV : n_views;
   using S = TileShape<NV>;
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ, VPT = S::VPT;
@@ -359,10 +361,15 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
       if (v >= N || rpass[v] != pass) continue;
       // branch-free: voxel-views that sample nothing read the zero slots with zero weights
       float a[G], bq[G], cq[G], d[G];
-      unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k]), a);
-      unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k] + 16), bq);
-      unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k]), cq);
-      unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k] + 16), d);
+      if (ablate & 4) {
+#pragma unroll
+        for (int ch = 0; ch < G; ++ch) a[ch] = bq[ch] = cq[ch] = d[ch] = __uint_as_float(anw[v][k] + asw[v][k] + ch);
+      } else {
+        unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k]), a);
+        unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k] + 16), bq);
+        unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k]), cq);
+        unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k] + 16), d);
+      }
 #pragma unroll
       for (int ch = 0; ch < G; ++ch)
         sv[ch][v] = __builtin_fmaf(d[ch], w[v][k][3], __builtin_fmaf(cq[ch], w[v][k][2],
@@ -376,7 +383,9 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
       const int c = c0 + ch;
       if (c >= C) break;
       const uint32_t soff = uint32_t(c) * uint32_t(nvox) * uint32_t(sizeof(TOut));
-      buf_store<TOut>(aggregate_fast<AGG, NV>(sv[ch], N, cfb ? cfb + c : nullptr, C), ors, ooff[k], soff);
+      const float r = aggregate_fast<AGG, NV>(sv[ch], N, cfb ? cfb + c : nullptr, C);
+      if (ablate & 1) asm volatile("" ::"v"(r));
+      else buf_store<TOut>(r, ors, ooff[k], soff);
     }
   };
 
@@ -399,9 +408,15 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
     auto issue = [&](int c0) {
 #pragma unroll
       for (int i = 0; i < MS; ++i)
-        if (t + kThreads * i < total)
+        if (t + kThreads * i < total) {
+          if (ablate & 2) {
 #pragma unroll
-          for (int k = 0; k < G; ++k) pre[i][k] = buf_load<TIn>(frs, goff[i], uint32_t((c0 + k) * HW * int(sizeof(TIn))));
+            for (int k = 0; k < G; ++k) pre[i][k] = goff[i] + c0 + k;
+          } else {
+#pragma unroll
+            for (int k = 0; k < G; ++k) pre[i][k] = buf_load<TIn>(frs, goff[i], uint32_t((c0 + k) * HW * int(sizeof(TIn))));
+          }
+        }
     };
     auto commit = [&](uint4* buf) {
 #pragma unroll
@@ -480,6 +495,8 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
   // lowers it (tests force the multi-pass and global-gather paths with it).
   int budget = 1 << 30;
   if (const char* e = getenv("MVN_UNPROJECT_LDS_SLOTS")) budget = max(1, atoi(e));
+  int ablate = 0;
+  if (const char* e = getenv("MVN_UNPROJECT_ABLATE")) ablate = atoi(e);
   auto blocks = [&](auto shape) {
     using S = decltype(shape);
     return (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) * ((Vz + S::TZ - 1) / S::TZ);
@@ -490,7 +507,7 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
     if (nb > INT_MAX) return false;
     unproject_tiled<AGG, TIn, TOut, NV, decltype(exact)::value><<<int(nb), kThreads, 0, s>>>(
         static_cast<const TIn*>(feat), P, coords, conf, static_cast<TOut*>(out), B, N, C, H, W, Vx, Vy, Vz,
-        align_corners, budget);
+        align_corners, budget, ablate);
     return true;
   };
   using I4 = std::integral_constant<int, 4>;

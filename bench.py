@@ -57,6 +57,26 @@ def frame_bytes(c, E):
             + 4 * (2 * 3 * V3) + 4 * (12 * c["views"] + 3 * c["joints"]))
 
 
+def measured_traffic(cfg_name):
+    """HBM bytes per unprojection launch from the newest committed PMC summary
+    (profiles/rNN_traffic.json, written by tools/profile_summary.py from rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes over the same kernel and config), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    for k, d in data.get(f"cfg{cfg_name}", {}).items():
+        if k.startswith("unproject_tiled<2,") and "hbm_bytes_per_launch" in d:
+            return d["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
+def kernel_name(c):
+    t = "float" if c["dtype"] == torch.float32 else "bf16"
+    return f"unproject_tiled<softmax, {t}, {t}, {4 if c['views'] <= 4 else 8} views>"
+
+
 def dtype_name(dt):
     return {torch.float32: "f32", torch.bfloat16: "bf16"}[dt]
 
@@ -177,6 +197,7 @@ def main():
 
     if rank == 0:
         r, c = main_res, main_res["cfg"]
+        traffic, traffic_src = measured_traffic(args.config)
         line = {
             "metric": METRIC,
             "value": r["fps"],
@@ -194,9 +215,10 @@ def main():
                        "views": c["views"], "channels": c["channels"], "heatmap": c["heatmap"],
                        "volume": c["volume"], "joints": c["joints"], "parallelism": f"dp{world}",
                        "collective": "all_gather joints (RCCL)" if world > 1 else None},
-            "roofline": {"kernel": "unproject_regviews<softmax>", "bound": "hbm",
+            "roofline": {"kernel": kernel_name(c), "bound": "hbm",
                          "achieved": r["achieved_gbps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": r["achieved_gbps"] / HBM_PEAK_GBPS, "traffic": None,
+                         "frac": r["achieved_gbps"] / HBM_PEAK_GBPS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "launch_ms": r["unproject_ms"], "algorithmic_bytes_per_launch": r["launch_bytes"]},
             "path_algorithmic_gbps": r["path_gbps"],
             "cpu_baseline": base,

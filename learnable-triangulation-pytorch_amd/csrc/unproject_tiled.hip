@@ -6,11 +6,13 @@
 // Why: a lane per voxel gathering its 4 taps per (view, channel) straight from the NCHW
 // maps touches a different cache line per lane (neighbouring z-voxels project ~1.6 px
 // apart, i.e. onto different image rows), so gathers run at L1/L2 request rate, not
-// bandwidth.  Here a block owns a compact 8x8x8 voxel tile.  Once per block it
+// bandwidth.  Here a block owns a compact voxel tile (4x8x16 for up to 4 views, z
+// fastest so that a wave's stores are 64-byte runs).  Once per block it
 //   1. projects its voxels in every view (geometry kept in registers),
-//   2. reduces per view the bounding box of the bilinear footprints (+1 px each way) and
-//      lays the N boxes out in LDS channels-last, 16 bytes per pixel (4 f32 / 8 bf16
-//      channels), with an odd row pitch so that z-neighbouring lanes spread over banks,
+//   2. reduces per view the bounding box of the bilinear footprints (+1 px each way; DPP
+//      wave reductions) and lays the N boxes out in LDS channels-last, 16 bytes per pixel
+//      (4 f32 channels; bf16 maps are widened when staged), with an odd row pitch so that
+//      z-neighbouring lanes spread over banks,
 //   3. turns every LDS pixel slot this thread stages into one byte offset into the
 //      frame's NCHW maps (or an out-of-range offset for pixels outside the image).
 // Then per group of G channels staging is only buffer loads — whose hardware range check
@@ -27,6 +29,7 @@
 // the cuboid) sends its block to direct global gathers.
 #include <stdlib.h>
 
+#include <climits>
 #include <utility>
 
 #include "unproject_common.hpp"
@@ -35,27 +38,41 @@ namespace mvn {
 namespace unproj {
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / kWave;
-// 16-byte LDS pixel slots per buffer (two buffers per block); the last 2 slots of each are
-// zero: the taps of voxel-views that sample nothing point there.
-template <int NV> struct Buf { static constexpr int slots = NV == 4 ? 1024 : 2048; };
+#ifndef MVN_STAGE_UNCOND
+#define MVN_STAGE_UNCOND 1   // stage every slot a thread owns (else skip slots past the footprint per wave)
+#endif
+
 constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any frame
 
-// Compile-time loop: f(std::integral_constant<int, i>) for i in [0, n).  Keeps per-voxel
-// register arrays statically indexed through the lambdas (no scratch demotion).
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int n, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, n>{});
-}
+// Tile of voxels per block (z fastest: a wave's output stores are 16-voxel = 64-byte runs
+// of a channel plane) and 16-byte LDS pixel slots per staging buffer (two per block; the
+// last 2 slots of each hold zeros: the taps of voxel-views that sample nothing point there).
+//   4 views: 4x8x16 tile, 512 threads, 2048 slots = 2 x 32 KiB (footprints of such tiles
+//            take ~2.2 slots / voxel)
+//   8 views: 2x8x16 tile, 256 threads, 2048 slots
+template <int NV> struct TileShape;
+// WAVES: waves per SIMD the register allocation must allow (4: two 512-thread blocks per CU).
+template <> struct TileShape<4> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, WAVES = 4; };
+template <> struct TileShape<8> { static constexpr int TX = 2, TY = 8, TZ = 16, THREADS = 256, SLOTS = 2048, WAVES = 2; };
 
-template <int NV> struct TileShape;               // tile dims and voxels per thread
-template <> struct TileShape<4> { static constexpr int TX = 4, TY = 8, TZ = 8, VPT = 1; };
-template <> struct TileShape<8> { static constexpr int TX = 4, TY = 8, TZ = 8, VPT = 1; };
+// Wave-wide integer min / max, returned wave-uniform.  row_shr DPP steps (identity
+// shifted in) leave each row's reduction in its lane 15; four readlanes combine the rows.
+__device__ __forceinline__ int wave_min_u(int v) {
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xf, 0xf, false));
+  return min(min(__builtin_amdgcn_readlane(v, 15), __builtin_amdgcn_readlane(v, 31)),
+             min(__builtin_amdgcn_readlane(v, 47), __builtin_amdgcn_readlane(v, 63)));
+}
+__device__ __forceinline__ int wave_max_u(int v) {
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));
+  return max(max(__builtin_amdgcn_readlane(v, 15), __builtin_amdgcn_readlane(v, 31)),
+             max(__builtin_amdgcn_readlane(v, 47), __builtin_amdgcn_readlane(v, 63)));
+}
 
 // Buffer descriptor from block-uniform inputs, provably in SGPRs (cdna_hip_programming.md T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
@@ -82,21 +99,14 @@ template <> __device__ __forceinline__ void buf_store<uint16_t>(float x, __amdgp
   __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, 0);
 }
 
-// 16-byte slot <-> G floats
+// LDS slots hold 4 f32 channels whatever the input dtype: bf16 maps are widened once
+// when staged (each staged pixel is read ~7 times by the tile's taps), not per tap.
 __device__ __forceinline__ void unpack(const uint4& q, float (&v)[4]) {
   v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
 }
-__device__ __forceinline__ void unpack(const uint4& q, float (&v)[8]) {
-  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    v[2 * k] = __uint_as_float(w[k] << 16);
-    v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
-  }
-}
-template <int G> __device__ __forceinline__ uint4 pack(const uint32_t (&b)[G]) {
-  if constexpr (G == 4) return make_uint4(b[0], b[1], b[2], b[3]);
-  else return make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
+template <typename TIn> __device__ __forceinline__ uint4 pack(const uint32_t (&b)[4]) {
+  if constexpr (sizeof(TIn) == 4) return make_uint4(b[0], b[1], b[2], b[3]);
+  else return make_uint4(b[0] << 16, b[1] << 16, b[2] << 16, b[3] << 16);   // bf16 -> f32 bits
 }
 
 // View aggregation, fast form for the staged path.  sum / max / conf are the reference's
@@ -183,18 +193,17 @@ __device__ __forceinline__ void gather_voxel(const TIn* __restrict__ fb, const f
 // NV = views held in registers (4 or 8); EXACT: the launch has exactly NV views, so every
 // per-view guard is a compile-time constant (no selects in the sampling / aggregation).
 template <int AGG, typename TIn, typename TOut, int NV, bool EXACT>
-__global__ __launch_bounds__(kThreads) void unproject_tiled(
+__global__ __launch_bounds__(TileShape<NV>::THREADS)
+__attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ conf, TOut* __restrict__ out, int B, int n_views, int C, int H, int W, int Vx,
-    int Vy, int Vz, int align_corners, int budget, int ablate) {
-  // ablate (diagnostics only, MVN_UNPROJECT_ABLATE): bit 0 skip the output stores, bit 1
-  // skip the staging loads, bit 2 skip the LDS tap reads (results are wrong; timing only)
+    int Vy, int Vz, int align_corners, int budget) {
   const int N = EXACT ? NV : n_views;
   using S = TileShape<NV>;
-  constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ, VPT = S::VPT;
-  static_assert(TX * TY * TZ == kThreads * VPT, "tile must give every thread VPT voxels");
-  constexpr int G = 16 / int(sizeof(TIn));            // channels per 16-byte slot
-  constexpr int kBuf = Buf<NV>::slots;
+  constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ, kThreads = S::THREADS, kBuf = S::SLOTS;
+  static_assert(TX * TY * TZ == kThreads, "one voxel per thread");
+  constexpr int kWaves = kThreads / kWave;
+  constexpr int G = 4;                                // f32 channels per 16-byte LDS slot
   constexpr int kZeroSlot = kBuf - 2;
   constexpr int MS = kBuf / kThreads;                 // staged slots per thread (max)
 
@@ -215,7 +224,6 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
   const int b = L / nTx;
 
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
-  const int lz = t % TZ, ly = (t / TZ) % TY, lx = t / (TZ * TY);
   const int nvox = Vx * Vy * Vz;
   const int HW = H * W;
   const float* Pb = P + size_t(b) * N * 12;
@@ -224,62 +232,43 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
 
   if (t < 4) stage[(t >> 1) * kBuf + kZeroSlot + (t & 1)] = make_uint4(0, 0, 0, 0);
 
-  // ---- voxels of this thread ------------------------------------------------------
-  int vox[VPT];
-  bool act[VPT];
-  float cx[VPT], cy[VPT], cz[VPT];
-#pragma unroll
-  for (int k = 0; k < VPT; ++k) {
-    const int X = tx * TX + lx + k * (TX / VPT), Y = ty * TY + ly, Z = tz * TZ + lz;
-    act[k] = (X < Vx) & (Y < Vy) & (Z < Vz);
-    vox[k] = act[k] ? (X * Vy + Y) * Vz + Z : 0;
-    const float* cp = coords + (size_t(b) * nvox + vox[k]) * 3;
-    cx[k] = cp[0]; cy[k] = cp[1]; cz[k] = cp[2];
-  }
+  // ---- this thread's voxel -----------------------------------------------------------
+  const int X = tx * TX + t / (TZ * TY), Y = ty * TY + (t / TZ) % TY, Z = tz * TZ + t % TZ;
+  const bool act = (X < Vx) & (Y < Vy) & (Z < Vz);
+  const int vox = act ? (X * Vy + Y) * Vz + Z : 0;
+  const float* cp = coords + (size_t(b) * nvox + vox) * 3;
+  const float cx = cp[0], cy = cp[1], cz = cp[2];
 
   // ---- per-view geometry: footprint base pixel, weights, "samples the image" flag --
-  int fx[NV][VPT], fy[NV][VPT];
-  float w[NV][VPT][4];
-  bool has[NV][VPT];
-  int bb[NV][4];                                      // thread-local xmin, xmax, ymin, ymax
+  int fx[NV], fy[NV];
+  float w[NV][4];
+  bool has[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    bb[v][0] = INT_MAX; bb[v][1] = INT_MIN; bb[v][2] = INT_MAX; bb[v][3] = INT_MIN;
-#pragma unroll
-    for (int k = 0; k < VPT; ++k) {
-      has[v][k] = false;
-      fx[v][k] = fy[v][k] = 0;
-      w[v][k][0] = w[v][k][1] = w[v][k][2] = w[v][k][3] = 0.f;
-      if (v < N) {
-        const Proj p = project(Pb + v * 12, cx[k], cy[k], cz[k], H, W, align_corners);
-        const float fx0 = floorf(p.ix), fy0 = floorf(p.iy);
-        // at least one of the 4 taps lies inside the image, and the voxel is in front
-        const bool h = act[k] & !p.invalid & (fx0 >= -1.f) & (fx0 < float(W)) & (fy0 >= -1.f) & (fy0 < float(H));
-        if (h) {
-          const float tx_ = p.ix - fx0, sx_ = 1.f - tx_, ty_ = p.iy - fy0, sy_ = 1.f - ty_;
-          w[v][k][0] = sy_ * sx_; w[v][k][1] = sy_ * tx_; w[v][k][2] = ty_ * sx_; w[v][k][3] = ty_ * tx_;
-          fx[v][k] = int(fx0); fy[v][k] = int(fy0);
-          bb[v][0] = min(bb[v][0], fx[v][k]); bb[v][1] = max(bb[v][1], fx[v][k]);
-          bb[v][2] = min(bb[v][2], fy[v][k]); bb[v][3] = max(bb[v][3], fy[v][k]);
-        }
-        has[v][k] = h;
+    has[v] = false;
+    fx[v] = fy[v] = 0;
+    w[v][0] = w[v][1] = w[v][2] = w[v][3] = 0.f;
+    if (v < N) {
+      const Proj p = project(Pb + v * 12, cx, cy, cz, H, W, align_corners);
+      const float fx0 = floorf(p.ix), fy0 = floorf(p.iy);
+      // at least one of the 4 taps lies inside the image, and the voxel is in front
+      const bool h = act & !p.invalid & (fx0 >= -1.f) & (fx0 < float(W)) & (fy0 >= -1.f) & (fy0 < float(H));
+      if (h) {
+        const float tx_ = p.ix - fx0, sx_ = 1.f - tx_, ty_ = p.iy - fy0, sy_ = 1.f - ty_;
+        w[v][0] = sy_ * sx_; w[v][1] = sy_ * tx_; w[v][2] = ty_ * sx_; w[v][3] = ty_ * tx_;
+        fx[v] = int(fx0); fy[v] = int(fy0);
       }
+      has[v] = h;
     }
   }
 
   // ---- block bounding boxes -> LDS regions ------------------------------------------
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      bb[v][0] = min(bb[v][0], __shfl_xor(bb[v][0], o, kWave));
-      bb[v][1] = max(bb[v][1], __shfl_xor(bb[v][1], o, kWave));
-      bb[v][2] = min(bb[v][2], __shfl_xor(bb[v][2], o, kWave));
-      bb[v][3] = max(bb[v][3], __shfl_xor(bb[v][3], o, kWave));
-    }
-    if (lane == 0) {
-      red[wid][v][0] = bb[v][0]; red[wid][v][1] = bb[v][1]; red[wid][v][2] = bb[v][2]; red[wid][v][3] = bb[v][3];
-    }
+    if (v >= N) break;
+    const int x0 = wave_min_u(has[v] ? fx[v] : INT_MAX), x1 = wave_max_u(has[v] ? fx[v] : INT_MIN);
+    const int y0 = wave_min_u(has[v] ? fy[v] : INT_MAX), y1 = wave_max_u(has[v] ? fy[v] : INT_MIN);
+    if (lane == 0) { red[wid][v][0] = x0; red[wid][v][1] = x1; red[wid][v][2] = y0; red[wid][v][3] = y1; }
   }
   __syncthreads();
   if (t == 0) {
@@ -328,70 +317,61 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
 
   if (npass < 0) {
     // A single footprint exceeds the LDS buffer: gather straight from global memory.
-#pragma unroll
-    for (int k = 0; k < VPT; ++k)
-      if (act[k])
-        gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + vox[k], nvox, N, C, H, W,
-                                     cx[k], cy[k], cz[k], align_corners);
+    if (act)
+      gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + vox, nvox, N, C, H, W, cx, cy, cz,
+                                   align_corners);
     return;
   }
 
   const __amdgpu_buffer_rsrc_t frs = make_rsrc(fb, uint32_t(size_t(N) * C * HW * sizeof(TIn)));
   const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + size_t(b) * C * nvox, uint32_t(size_t(C) * nvox * sizeof(TOut)));
-  uint32_t ooff[VPT];
-#pragma unroll
-  for (int k = 0; k < VPT; ++k) ooff[k] = act[k] ? uint32_t(vox[k]) * uint32_t(sizeof(TOut)) : kOob;
+  const uint32_t ooff = act ? uint32_t(vox) * uint32_t(sizeof(TOut)) : kOob;
 
-  // LDS byte offsets of each voxel-view's north-west and south-west taps (buffer 0)
-  uint32_t anw[NV][VPT], asw[NV][VPT];
+  // LDS byte offsets of each view's north-west and south-west taps (buffer 0)
+  uint32_t anw[NV], asw[NV];
 #pragma unroll
-  for (int v = 0; v < NV; ++v)
-#pragma unroll
-    for (int k = 0; k < VPT; ++k) {
-      const int slot = rbase[v] + (fy[v][k] - ry[v]) * rpitch[v] + (fx[v][k] - rx[v]);
-      anw[v][k] = uint32_t(has[v][k] ? slot : kZeroSlot) * 16u;
-      asw[v][k] = uint32_t(has[v][k] ? slot + rpitch[v] : kZeroSlot) * 16u;
-    }
+  for (int v = 0; v < NV; ++v) {
+    const int slot = rbase[v] + (fy[v] - ry[v]) * rpitch[v] + (fx[v] - rx[v]);
+    anw[v] = uint32_t(has[v] ? slot : kZeroSlot) * 16u;
+    asw[v] = uint32_t(has[v] ? slot + rpitch[v] : kZeroSlot) * 16u;
+  }
 
-  // sample voxel k's views of `pass` from an LDS buffer into sv[ch][v]
-  auto sample_voxel = [&](const char* buf, int pass, auto kc, float (&sv)[G][NV]) {
-    constexpr int k = decltype(kc)::value;
+  // sample the views staged in an LDS buffer (ONE_PASS: all of them; else those of `pass`)
+  auto sample_views = [&](const char* buf, auto one_pass, int pass, float (&sv)[G][NV]) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      if (v >= N || rpass[v] != pass) continue;
+      if (v >= N) continue;
+      if (!decltype(one_pass)::value && rpass[v] != pass) continue;
       // branch-free: voxel-views that sample nothing read the zero slots with zero weights
       float a[G], bq[G], cq[G], d[G];
-      if (ablate & 4) {
-#pragma unroll
-        for (int ch = 0; ch < G; ++ch) a[ch] = bq[ch] = cq[ch] = d[ch] = __uint_as_float(anw[v][k] + asw[v][k] + ch);
-      } else {
-        unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k]), a);
-        unpack(*reinterpret_cast<const uint4*>(buf + anw[v][k] + 16), bq);
-        unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k]), cq);
-        unpack(*reinterpret_cast<const uint4*>(buf + asw[v][k] + 16), d);
-      }
+      unpack(*reinterpret_cast<const uint4*>(buf + anw[v]), a);
+      unpack(*reinterpret_cast<const uint4*>(buf + anw[v] + 16), bq);
+      unpack(*reinterpret_cast<const uint4*>(buf + asw[v]), cq);
+      unpack(*reinterpret_cast<const uint4*>(buf + asw[v] + 16), d);
 #pragma unroll
       for (int ch = 0; ch < G; ++ch)
-        sv[ch][v] = __builtin_fmaf(d[ch], w[v][k][3], __builtin_fmaf(cq[ch], w[v][k][2],
-                    __builtin_fmaf(bq[ch], w[v][k][1], a[ch] * w[v][k][0])));
+        sv[ch][v] = __builtin_fmaf(d[ch], w[v][3], __builtin_fmaf(cq[ch], w[v][2],
+                    __builtin_fmaf(bq[ch], w[v][1], a[ch] * w[v][0])));
+      if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight
     }
   };
-  auto aggregate_store = [&](int c0, auto kc, const float (&sv)[G][NV]) {
-    constexpr int k = decltype(kc)::value;
+  auto aggregate_store = [&](int c0, const float (&sv)[G][NV]) {
 #pragma unroll
     for (int ch = 0; ch < G; ++ch) {
       const int c = c0 + ch;
       if (c >= C) break;
       const uint32_t soff = uint32_t(c) * uint32_t(nvox) * uint32_t(sizeof(TOut));
-      const float r = aggregate_fast<AGG, NV>(sv[ch], N, cfb ? cfb + c : nullptr, C);
-      if (ablate & 1) asm volatile("" ::"v"(r));
-      else buf_store<TOut>(r, ors, ooff[k], soff);
+      buf_store<TOut>(aggregate_fast<AGG, NV>(sv[ch], N, cfb ? cfb + c : nullptr, C), ors, ooff, soff);
     }
   };
 
   if (npass == 1) {
     // ---- fast path: one pass, staging descriptors in registers, two LDS buffers -----
-    const int total = block_info[1];
+    // Slot t + kThreads * i is staged by this thread.  The guard is per WAVE (scalar
+    // branch): lanes past `total` load from the out-of-range offset and write zeros
+    // into unused slots (never the zero slots' neighbours in use: total <= kZeroSlot).
+    const int total = __builtin_amdgcn_readfirstlane(block_info[1]);
+    const int wfirst = __builtin_amdgcn_readfirstlane(wid * kWave);
     uint32_t goff[MS];
 #pragma unroll
     for (int i = 0; i < MS; ++i) {
@@ -405,31 +385,25 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
       goff[i] = in ? uint32_t((q.v * C * HW + gy * W + gx) * int(sizeof(TIn))) : kOob;
     }
     uint32_t pre[MS][G];
+    constexpr bool UNCOND = MVN_STAGE_UNCOND;
     auto issue = [&](int c0) {
 #pragma unroll
       for (int i = 0; i < MS; ++i)
-        if (t + kThreads * i < total) {
-          if (ablate & 2) {
+        if (UNCOND || wfirst + kThreads * i < total) {
 #pragma unroll
-            for (int k = 0; k < G; ++k) pre[i][k] = goff[i] + c0 + k;
-          } else {
-#pragma unroll
-            for (int k = 0; k < G; ++k) pre[i][k] = buf_load<TIn>(frs, goff[i], uint32_t((c0 + k) * HW * int(sizeof(TIn))));
-          }
+          for (int k = 0; k < G; ++k) pre[i][k] = buf_load<TIn>(frs, goff[i], uint32_t((c0 + k) * HW * int(sizeof(TIn))));
         }
     };
     auto commit = [&](uint4* buf) {
 #pragma unroll
       for (int i = 0; i < MS; ++i)
-        if (t + kThreads * i < total) buf[t + kThreads * i] = pack<G>(pre[i]);
+        if (UNCOND || wfirst + kThreads * i < total) buf[t + kThreads * i] = pack<TIn>(pre[i]);
     };
     auto consume = [&](const uint4* buf, int c0) {
-      static_for<VPT>([&](auto kc) {         // one voxel at a time bounds the LDS reads in flight
-        float sv[G][NV];
-        sample_voxel(reinterpret_cast<const char*>(buf), 0, kc, sv);
-        aggregate_store(c0, kc, sv);
-        __builtin_amdgcn_sched_barrier(0);
-      });
+      float sv[G][NV];
+      sample_views(reinterpret_cast<const char*>(buf), std::true_type{}, 0, sv);
+      aggregate_store(c0, sv);
+      __builtin_amdgcn_sched_barrier(0);     // bounds the LDS reads in flight (registers)
     };
 
     issue(0);
@@ -453,7 +427,7 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
 
   // ---- several passes per channel group (close cameras): stage, sample, repeat -------
   for (int c0 = 0; c0 < C; c0 += G) {
-    float sv[VPT][G][NV];
+    float sv[G][NV];
     for (int pass = 0; pass < npass; ++pass) {
       int total = 0;
 #pragma unroll
@@ -469,16 +443,13 @@ __global__ __launch_bounds__(kThreads) void unproject_tiled(
         uint32_t bits[G];
 #pragma unroll
         for (int k = 0; k < G; ++k) bits[k] = buf_load<TIn>(frs, go, uint32_t((c0 + k) * HW * int(sizeof(TIn))));
-        stage[idx] = pack<G>(bits);
+        stage[idx] = pack<TIn>(bits);
       }
       __syncthreads();
-      static_for<VPT>([&](auto kc) {
-        sample_voxel(reinterpret_cast<const char*>(stage), pass, kc, sv[decltype(kc)::value]);
-        __builtin_amdgcn_sched_barrier(0);
-      });
+      sample_views(reinterpret_cast<const char*>(stage), std::false_type{}, pass, sv);
       __syncthreads();
     }
-    static_for<VPT>([&](auto kc) { aggregate_store(c0, kc, sv[decltype(kc)::value]); });
+    aggregate_store(c0, sv);
   }
 }
 
@@ -495,19 +466,15 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
   // lowers it (tests force the multi-pass and global-gather paths with it).
   int budget = 1 << 30;
   if (const char* e = getenv("MVN_UNPROJECT_LDS_SLOTS")) budget = max(1, atoi(e));
-  int ablate = 0;
-  if (const char* e = getenv("MVN_UNPROJECT_ABLATE")) ablate = atoi(e);
-  auto blocks = [&](auto shape) {
-    using S = decltype(shape);
-    return (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) * ((Vz + S::TZ - 1) / S::TZ);
-  };
   auto go = [&](auto nv, auto exact) {
     constexpr int NV = decltype(nv)::value;
-    const long long nb = blocks(TileShape<NV>{});
+    using S = TileShape<NV>;
+    const long long nb = (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) *
+                         ((Vz + S::TZ - 1) / S::TZ);
     if (nb > INT_MAX) return false;
-    unproject_tiled<AGG, TIn, TOut, NV, decltype(exact)::value><<<int(nb), kThreads, 0, s>>>(
+    unproject_tiled<AGG, TIn, TOut, NV, decltype(exact)::value><<<int(nb), S::THREADS, 0, s>>>(
         static_cast<const TIn*>(feat), P, coords, conf, static_cast<TOut*>(out), B, N, C, H, W, Vx, Vy, Vz,
-        align_corners, budget, ablate);
+        align_corners, budget);
     return true;
   };
   using I4 = std::integral_constant<int, 4>;

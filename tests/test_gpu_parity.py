@@ -74,7 +74,7 @@ def tile_footprints(proj, coords, H, W, tile):
                         m = ok[b, v, x:x + TX, y:y + TY, z:z + TZ]
                         a = fx[b, v, x:x + TX, y:y + TY, z:z + TZ][m]
                         c = fy[b, v, x:x + TX, y:y + TY, z:z + TZ][m]
-                        areas.append(0 if a.size == 0 else int((a.max() - a.min() + 2) * (c.max() - c.min() + 2)))
+                        areas.append(0 if a.size == 0 else int((int(a.max() - a.min() + 2) | 1) * (c.max() - c.min() + 2)))
                     out.append(areas)
     return np.array(out)
 
@@ -87,7 +87,7 @@ def test_unproject_every_kernel_path(device, monkeypatch, path, method):
     from mvn_rocm import synth
     vb = synth.volumetric_batch(2, n_views=4, channels=10, heatmap=64, volume=32, seed=31)
     feat, proj, coords = vb.features.numpy(), vb.proj.numpy(), vb.coords.numpy()
-    areas = tile_footprints(proj, coords, 64, 64, (8, 8, 8))
+    areas = tile_footprints(proj, coords, 64, 64, (4, 8, 16))     # TileShape<4> in unproject_tiled.hip
     if path == "lds_multipass":        # every footprint fits alone, no tile's views fit together
         budget = int(areas.max()) + 64        # margin: the kernel rounds in f32
         assert (areas.sum(1) + 1 > budget).any()

@@ -5,7 +5,7 @@ import sys
 
 src = sys.argv[1]
 extra = sys.argv[2:]
-cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
        "-I/root/repo/include", "-I/root/repo/learnable-triangulation-pytorch_amd/csrc", "-c", src, "-o", "/tmp/_kr.o",
        "-Rpass-analysis=kernel-resource-usage"] + extra
 out = subprocess.run(cmd, capture_output=True, text=True).stderr

@@ -1,0 +1,74 @@
+"""Turn tools/profile_round.sh output into the committed profiles/ files.
+
+    python tools/profile_summary.py <round-tag>
+writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, mvn kernels), profiles/<tag>_traffic.json
+(per config and kernel: mean FETCH_SIZE / WRITE_SIZE per dispatch; HBM bytes = 2 x FETCH + WRITE,
+MI355X_MICROARCH.md 'HBM': gfx950 FETCH_SIZE counts half the bytes of wide streaming reads) and
+profiles/<tag>_sq_cfg2.txt (SQ instruction mix of the unprojection).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+raw = os.path.join(ROOT, "gpurun_out", tag)
+dst = os.path.join(ROOT, "profiles")
+os.makedirs(dst, exist_ok=True)
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("mvn::", "").replace("(anonymous namespace)::", "") \
+        .replace("unproj::", "").replace("unsigned short", "bf16")
+
+
+# 1. kernel stats
+stats = glob.glob(os.path.join(raw, "kt", "**", "*kernel_stats.csv"), recursive=True)
+rows = [r for f in stats for r in csv.DictReader(open(f))]
+with open(os.path.join(dst, f"{tag}_kernel_stats.csv"), "w", newline="") as fo:
+    w = csv.writer(fo)
+    w.writerow(["kernel", "calls", "avg_us", "min_us", "max_us", "pct_of_gpu_time"])
+    for r in rows:
+        w.writerow([short(r["Name"]), r["Calls"], f"{float(r['AverageNs']) / 1e3:.2f}",
+                    f"{float(r['MinNs']) / 1e3:.2f}", f"{float(r['MaxNs']) / 1e3:.2f}", r["Percentage"]])
+
+# 2. traffic
+traffic = {}
+for cfg in ("2", "3"):
+    per = defaultdict(dict)
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        vals = defaultdict(list)
+        for f in glob.glob(os.path.join(raw, f"pmc_{c}_cfg{cfg}", "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r["Counter_Name"] == c:
+                    vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+        for k, v in vals.items():
+            per[k][c.lower() + "_kib"] = sum(v) / len(v)
+            per[k]["dispatches"] = len(v)
+    for k, d in per.items():
+        if "fetch_size_kib" in d and "write_size_kib" in d:
+            d["hbm_bytes_per_launch"] = (2 * d["fetch_size_kib"] + d["write_size_kib"]) * 1024
+    traffic[f"cfg{cfg}"] = per
+traffic["_note"] = ("rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes over tools/prof_unproject.py; "
+                    "HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), MI355X_MICROARCH.md 'HBM' gfx950 rule")
+json.dump(traffic, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1, sort_keys=True)
+
+# 3. SQ mix
+vals = defaultdict(lambda: defaultdict(list))
+for f in glob.glob(os.path.join(raw, "sq_cfg2", "p*", "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        vals[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+with open(os.path.join(dst, f"{tag}_sq_cfg2.txt"), "w") as fo:
+    for k, d in vals.items():
+        fo.write(k + "\n")
+        waves = sum(d["SQ_WAVES"]) / len(d["SQ_WAVES"]) if "SQ_WAVES" in d else None
+        for c in sorted(d):
+            m = sum(d[c]) / len(d[c])
+            per = f"   per wave {m / waves:12.1f}" if waves else ""
+            fo.write(f"   {c:28s} {m:16.1f}{per}\n")
+print(open(os.path.join(dst, f"{tag}_kernel_stats.csv")).read())
+print(json.dumps(traffic, indent=1))
+print(open(os.path.join(dst, f"{tag}_sq_cfg2.txt")).read())

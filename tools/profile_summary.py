@@ -21,8 +21,9 @@ os.makedirs(dst, exist_ok=True)
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").replace("mvn::", "").replace("(anonymous namespace)::", "") \
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "").replace("mvn::", "") \
         .replace("unproj::", "").replace("unsigned short", "bf16")
+    return name.split("(")[0]
 
 
 # 1. kernel stats

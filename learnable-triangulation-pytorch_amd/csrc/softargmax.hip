@@ -6,9 +6,9 @@
 // The caller's `volumes * volume_multiplier` (triangulation.py:353) is fused.
 //
 // Three stream-ordered launches (the middle one tiny):
-//   pass 1  softargmax_partials : one wave per (2048-voxel chunk, joint, frame) streams
-//           the chunk once and reduces (max, sum e, sum e*x, sum e*y, sum e*z) with wave
-//           shuffles into one 5-float partial; no barriers, no LDS.
+//   pass 1  softargmax_partials : one wave per (512-voxel chunk, frame) holds the chunk's
+//           coordinates and loops over the joints, reducing (max, sum e, sum e*x, sum e*y,
+//           sum e*z) per joint with DPP into one 5-float partial; no barriers, no LDS.
 //   pass 2  softargmax_combine  : one wave per (frame, joint) folds the partials (online
 //           rescale), writes the coordinates and (max, 1/sum).
 //   pass 3  softargmax_finalize : one block per (4096-voxel chunk, joint, frame) streams
@@ -22,7 +22,7 @@ constexpr int kSaBlock = 256;
 constexpr int kSaVpt = 16;                      // voxels per thread
 constexpr int kSaChunk = kSaBlock * kSaVpt;     // 4096 voxels per block
 constexpr int kPartial = 5;                     // m, s, sx, sy, sz
-constexpr int kPartChunk = 2048;                // voxels per pass-1 wave
+constexpr int kPartChunk = 512;                 // voxels per pass-1 wave (all joints)
 
 template <typename T> struct Vec;
 template <> struct Vec<float> { static constexpr int n = 4; };
@@ -95,84 +95,117 @@ __device__ __forceinline__ void wave_merge(float& m, float& s, float& sx, float&
   }
 }
 
-// Pass 1: one WAVE per (frame, joint, 2048-voxel chunk) — no barriers, no LDS.  Each lane
-// streams 32 voxels as vector runs, keeps an online (max, sum e, sum e*xyz) and the wave
-// merges the lanes once.  Coordinates are re-read per joint from L2 (they are 12 B per
-// voxel against 2-4 B of volume; L2 absorbs the re-reads, HBM sees them once).
+// Wave reductions: row_shr DPP steps, then row_bcast:15 / row_bcast:31; the result is
+// valid in lane 63 (6 DPP-fused VALU ops each).
+template <int CTRL, int RMASK> __device__ __forceinline__ float dpp_f(float v, float ident) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(ident), __float_as_int(v), CTRL, RMASK, 0xf, false));
+}
+__device__ __forceinline__ float wave_max63(float v) {
+  constexpr float I = -INFINITY;
+  v = fmaxf(v, dpp_f<0x111, 0xf>(v, I)); v = fmaxf(v, dpp_f<0x112, 0xf>(v, I));
+  v = fmaxf(v, dpp_f<0x114, 0xf>(v, I)); v = fmaxf(v, dpp_f<0x118, 0xf>(v, I));
+  v = fmaxf(v, dpp_f<0x142, 0xa>(v, I)); v = fmaxf(v, dpp_f<0x143, 0xc>(v, I));
+  return v;
+}
+__device__ __forceinline__ float wave_sum63(float v) {
+  v += dpp_f<0x111, 0xf>(v, 0.f); v += dpp_f<0x112, 0xf>(v, 0.f);
+  v += dpp_f<0x114, 0xf>(v, 0.f); v += dpp_f<0x118, 0xf>(v, 0.f);
+  v += dpp_f<0x142, 0xa>(v, 0.f); v += dpp_f<0x143, 0xc>(v, 0.f);
+  return v;
+}
+
+// Pass 1: one WAVE per (frame, 512-voxel chunk), looping over ALL joints — no barriers,
+// no LDS.  The chunk's coordinates are loaded into registers once (12 B per voxel; one
+// wave per joint would re-read them J times), then per joint every lane loads its 16
+// voxels as vector runs (the next joint's loads are in flight during this joint's math),
+// the wave max is reduced first so that all lanes exponentiate against the same max
+// (plain additive sums, no per-lane rescaling), and (sum e, sum e*x, sum e*y, sum e*z)
+// are DPP-reduced into one 5-float partial per (frame, joint, chunk).
 template <typename T, bool SOFTMAX>
 __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     const T* __restrict__ vol, long long bstride, long long jstride, const float* __restrict__ coords,
     float mult, float* __restrict__ part, int J, int nvox, int nchunk, bool vec_ok) {
   constexpr int VEC = Vec<T>::n;
   constexpr int RUNS = kPartChunk / (kWave * VEC);
-  const int chunk = blockIdx.x, b = blockIdx.z;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const int j = blockIdx.y * (kSaBlock / kWave) + wid;
-  if (j >= J) return;                                  // whole wave; this kernel has no barriers
-  const T* vj = vol + b * bstride + j * jstride;
+  const int chunk = blockIdx.x * (kSaBlock / kWave) + wid, b = blockIdx.y;
+  if (chunk >= nchunk) return;                         // whole wave; this kernel has no barriers
+  const T* vb = vol + b * bstride;
   const float* cb = coords + size_t(b) * nvox * 3;
+  const float fill = SOFTMAX ? -INFINITY : 0.f;
 
-  // Loads are issued for a batch of runs before any arithmetic: the online-max chain
-  // would otherwise expose one memory latency per run.
-  constexpr int BATCH = VEC == 4 ? 4 : 2;            // ~64 loaded floats per batch
-  float m = SOFTMAX ? -INFINITY : 0.f, s = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
+  float c[RUNS][3 * VEC];
 #pragma unroll
-  for (int r0 = 0; r0 < RUNS; r0 += BATCH) {
-    float x[BATCH][VEC], c[BATCH][3 * VEC];
+  for (int r = 0; r < RUNS; ++r) {
+    const int i = chunk * kPartChunk + r * kWave * VEC + lane * VEC;
+    if (vec_ok && i + VEC <= nvox) {
+      const float4* cp = reinterpret_cast<const float4*>(cb + size_t(i) * 3);
 #pragma unroll
-    for (int q = 0; q < BATCH; ++q) {
-      const int i = chunk * kPartChunk + (r0 + q) * kWave * VEC + lane * VEC;
-      load_run<T, VEC>(vj, i, nvox, vec_ok, x[q], SOFTMAX ? -INFINITY : 0.f);
-      if (vec_ok && i + VEC <= nvox) {
-        const float4* cp = reinterpret_cast<const float4*>(cb + size_t(i) * 3);
-#pragma unroll
-        for (int u = 0; u < 3 * VEC / 4; ++u) {
-          const float4 f = cp[u];
-          c[q][4 * u] = f.x; c[q][4 * u + 1] = f.y; c[q][4 * u + 2] = f.z; c[q][4 * u + 3] = f.w;
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < 3 * VEC; ++u) c[q][u] = (i + u / 3 < nvox) ? cb[size_t(i) * 3 + u] : 0.f;
+      for (int u = 0; u < 3 * VEC / 4; ++u) {
+        const float4 f = cp[u];
+        c[r][4 * u] = f.x; c[r][4 * u + 1] = f.y; c[r][4 * u + 2] = f.z; c[r][4 * u + 3] = f.w;
       }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 3 * VEC; ++u) c[r][u] = (i + u / 3 < nvox) ? cb[size_t(i) * 3 + u] : 0.f;
     }
+  }
+  auto load = [&](int j, float (&x)[RUNS][VEC]) {
+#pragma unroll
+    for (int r = 0; r < RUNS; ++r)
+      load_run<T, VEC>(vb + j * jstride, chunk * kPartChunk + r * kWave * VEC + lane * VEC, nvox, vec_ok, x[r], fill);
+  };
+
+  float x[RUNS][VEC];
+  load(0, x);
+  for (int j = 0; j < J; ++j) {
+    float xn[RUNS][VEC];
+    if (j + 1 < J) load(j + 1, xn);
+    float m = 0.f, s = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
     if constexpr (SOFTMAX) {
-      float mr = m;
+      constexpr float kLog2e = 1.4426950408889634f;
+      float lm = -INFINITY;
 #pragma unroll
-      for (int q = 0; q < BATCH; ++q)
+      for (int r = 0; r < RUNS; ++r)
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) { x[q][k] = x[q][k] * mult; mr = fmaxf(mr, x[q][k]); }
-      if (mr != -INFINITY) {
-        const float kk = (m == -INFINITY) ? 0.f : __expf(m - mr);
-        s *= kk; sx *= kk; sy *= kk; sz *= kk;
-        m = mr;
+        for (int k = 0; k < VEC; ++k) { x[r][k] = x[r][k] * mult; lm = fmaxf(lm, x[r][k]); }
+      m = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wave_max63(lm)), kWave - 1));
+      if (m != -INFINITY) {                            // wave-uniform
+        const float ml = m * kLog2e;
 #pragma unroll
-        for (int q = 0; q < BATCH; ++q)
+        for (int r = 0; r < RUNS; ++r)
 #pragma unroll
           for (int k = 0; k < VEC; ++k) {
-            const float e = __expf(x[q][k] - mr);
+            const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(x[r][k], kLog2e, -ml));
             s += e;
-            sx = __builtin_fmaf(e, c[q][3 * k], sx);
-            sy = __builtin_fmaf(e, c[q][3 * k + 1], sy);
-            sz = __builtin_fmaf(e, c[q][3 * k + 2], sz);
+            sx = __builtin_fmaf(e, c[r][3 * k], sx);
+            sy = __builtin_fmaf(e, c[r][3 * k + 1], sy);
+            sz = __builtin_fmaf(e, c[r][3 * k + 2], sz);
           }
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < BATCH; ++q)
+      for (int r = 0; r < RUNS; ++r)
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-          const float e = fmaxf(x[q][k] * mult, 0.f);
+          const float e = fmaxf(x[r][k] * mult, 0.f);
           s += e;
-          sx = __builtin_fmaf(e, c[q][3 * k], sx);
-          sy = __builtin_fmaf(e, c[q][3 * k + 1], sy);
-          sz = __builtin_fmaf(e, c[q][3 * k + 2], sz);
+          sx = __builtin_fmaf(e, c[r][3 * k], sx);
+          sy = __builtin_fmaf(e, c[r][3 * k + 1], sy);
+          sz = __builtin_fmaf(e, c[r][3 * k + 2], sz);
         }
     }
-  }
-  wave_merge<SOFTMAX>(m, s, sx, sy, sz);
-  if (lane == 0) {
-    float* o = part + ((size_t(b) * J + j) * nchunk + chunk) * kPartial;
-    o[0] = m; o[1] = s; o[2] = sx; o[3] = sy; o[4] = sz;
+    s = wave_sum63(s); sx = wave_sum63(sx); sy = wave_sum63(sy); sz = wave_sum63(sz);
+    if (lane == kWave - 1) {
+      float* o = part + ((size_t(b) * J + j) * nchunk + chunk) * kPartial;
+      o[0] = m; o[1] = s; o[2] = sx; o[3] = sy; o[4] = sz;
+    }
+    if (j + 1 < J) {
+#pragma unroll
+      for (int r = 0; r < RUNS; ++r)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) x[r][k] = xn[r][k];
+    }
   }
 }
 
@@ -250,7 +283,7 @@ int launch(const void* vol, long long bs, long long js, const float* coords, flo
   const bool vec_ok = (reinterpret_cast<uintptr_t>(vol) % 16 == 0) && (bs * sizeof(T)) % 16 == 0 &&
                       (js * sizeof(T)) % 16 == 0 && (nvox % 8 == 0) &&
                       (out == nullptr || reinterpret_cast<uintptr_t>(out) % 16 == 0);
-  softargmax_partials<T, SOFTMAX><<<dim3(npart, (J + kSaBlock / kWave - 1) / (kSaBlock / kWave), B), kSaBlock, 0, st>>>(
+  softargmax_partials<T, SOFTMAX><<<dim3((npart + kSaBlock / kWave - 1) / (kSaBlock / kWave), B), kSaBlock, 0, st>>>(
       static_cast<const T*>(vol), bs, js, coords, mult, part, J, nvox, npart, vec_ok);
   if (!launch_ok()) return MVN_ERR_LAUNCH;
   float* stat = part + size_t(B) * J * npart * kPartial;

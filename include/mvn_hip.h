@@ -11,6 +11,8 @@
  *   mvn_softargmax3d     <- mvn/utils/op.py:84-96    integrate_tensor_3d_with_coordinates(...)
  *   mvn_dlt              <- mvn/utils/multiview.py:162-174 triangulate_batch_of_points(...)
  *                           (+ its per-point solver multiview.py:132-159)
+ *   mvn_softargmax2d     <- mvn/utils/op.py:11-47    integrate_tensor_2d(...)  (the algebraic
+ *                           path's producer of the DLT's 2D points)
  *
  * Conventions
  *   - Every buffer is caller-owned device memory (hipMalloc / torch), contiguous,
@@ -115,6 +117,17 @@ int mvn_softargmax3d(const void* vol, int vol_dtype,
  */
 int mvn_dlt(const float* proj, const float* pts, const float* conf, float* out,
             int B, int N, int J, void* stream);
+
+/*
+ * 2D soft-argmax of heatmaps.  Replaces mvn/utils/op.py:11-47 (integrate_tensor_2d) with
+ * the caller's `heatmaps * heatmap_multiplier` (triangulation.py:164) fused.
+ *   heatmaps  (B, J, H, W)  dtype (f32 | bf16), contiguous
+ *   out_xy    (B, J, 2)     f32: (x, y) = sum p * (w, h) / sum p  (op.py:31-42)
+ *   out_maps  (B, J, H, W)  out_dtype: softmax-normalised (softmax = 1) or relu'd maps
+ *                           (softmax = 0, not normalised, op.py:27); NULL = not wanted
+ */
+int mvn_softargmax2d(const void* heatmaps, int dtype, float multiplier, int softmax, float* out_xy,
+                     void* out_maps, int out_dtype, int B, int J, int H, int W, void* stream);
 
 /* ---- backward (autograd) ------------------------------------------------------------
  * Gradients of the three ops, replacing the ATen autograd the reference relies on

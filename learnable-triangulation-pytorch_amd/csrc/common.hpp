@@ -15,12 +15,15 @@ constexpr int kWave = 64;
 __device__ __forceinline__ float to_f32(float v) { return v; }
 __device__ __forceinline__ float to_f32(uint16_t v) { return __uint_as_float(uint32_t(v) << 16); }
 
-// Round-to-nearest-even f32 -> bf16 with NaN kept a NaN.
+// Round-to-nearest-even f32 -> bf16 (NaN stays NaN): gfx950's v_cvt_pk_bf16_f32.
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return uint16_t((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return uint16_t(u >> 16);
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
+}
+// Two values -> one dword (lo in bits 0-15): a single v_cvt_pk_bf16_f32.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 
 template <typename T> __device__ __forceinline__ void store_elem(T* p, float v);

@@ -58,7 +58,7 @@ __device__ __forceinline__ void store_run(T* __restrict__ p, int i, int nvox, bo
     } else {
       uint32_t w[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) w[k] = uint32_t(f32_to_bf16(v[2 * k])) | (uint32_t(f32_to_bf16(v[2 * k + 1])) << 16);
+      for (int k = 0; k < 4; ++k) w[k] = pack_bf16x2(v[2 * k], v[2 * k + 1]);
       *reinterpret_cast<uint4*>(p + i) = make_uint4(w[0], w[1], w[2], w[3]);
     }
   } else {

@@ -5,6 +5,7 @@ Drop-in replacements for the three hot-path functions of learnable-triangulation
     mvn_rocm.op.unproject_heatmaps                    <- mvn/utils/op.py:99-163
     mvn_rocm.op.integrate_tensor_3d_with_coordinates  <- mvn/utils/op.py:84-96
     mvn_rocm.multiview.triangulate_batch_of_points    <- mvn/utils/multiview.py:162-174
+    mvn_rocm.op.integrate_tensor_2d                   <- mvn/utils/op.py:11-47 (algebraic path)
 
 backed by hand-written gfx950 HIP kernels in libmvn_hip.so (C ABI: include/mvn_hip.h).
 ``install()`` rebinds them inside an importable ``mvn`` package so that
@@ -36,8 +37,10 @@ def install(mvn_op=None, mvn_multiview=None):
         "unproject_heatmaps": mvn_op.unproject_heatmaps,
         "integrate_tensor_3d_with_coordinates": mvn_op.integrate_tensor_3d_with_coordinates,
         "triangulate_batch_of_points": mvn_multiview.triangulate_batch_of_points,
+        "integrate_tensor_2d": mvn_op.integrate_tensor_2d,
     }
     mvn_op.unproject_heatmaps = op.unproject_heatmaps
     mvn_op.integrate_tensor_3d_with_coordinates = op.integrate_tensor_3d_with_coordinates
     mvn_multiview.triangulate_batch_of_points = multiview.triangulate_batch_of_points
+    mvn_op.integrate_tensor_2d = op.integrate_tensor_2d
     return previous

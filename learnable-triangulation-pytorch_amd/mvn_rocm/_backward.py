@@ -118,3 +118,40 @@ def dlt_backward(ctx, grad_out):
         return None, None, None
     gpts, gconf = dlt_bwd(proj, pts, conf, grad_out)
     return None, gpts if want_pts else None, gconf if want_conf else None
+
+
+def softargmax2d_backward(ctx, grad_xy, grad_maps):
+    """d/d(heatmaps) of op.integrate_tensor_2d, as GPU tensor algebra (the op is (B*N, J,
+    96, 96)-small; no kernel of its own).  With v = multiplier * h, e = exp(v - max) or
+    relu(v), S = sum e, p = e / S, (X, Y) = sum p * (w, h):
+      softmax: dL/dv = p * ((w - X) gX + (h - Y) gY + g_map - sum(g_map * p))
+      relu:    dL/dv = [v > 0] * (((w - X) gX + (h - Y) gY) / S + g_map)
+    """
+    hm, xy = ctx.saved_tensors
+    softmax, mult = ctx.cfg
+    v = hm.float() * mult
+    B, J, H, W = v.shape
+    ws = torch.arange(W, dtype=torch.float32, device=v.device).view(1, 1, 1, W)
+    hs = torch.arange(H, dtype=torch.float32, device=v.device).view(1, 1, H, 1)
+    X, Y = xy[..., 0:1, None], xy[..., 1:2, None]
+    gx = grad_xy[..., 0:1, None] if grad_xy is not None else None
+    gy = grad_xy[..., 1:2, None] if grad_xy is not None else None
+    geo = torch.zeros_like(v)
+    if grad_xy is not None:
+        geo = (ws - X) * gx + (hs - Y) * gy
+    has_gm = grad_maps is not None and grad_maps.numel() > 0
+    if softmax:
+        p = torch.softmax(v.flatten(2), dim=2).view_as(v)
+        g = geo
+        if has_gm:
+            gm = grad_maps.float()
+            g = g + gm - (gm * p).sum(dim=(2, 3), keepdim=True)
+        gv = p * g
+    else:
+        e = torch.relu(v)
+        S = e.sum(dim=(2, 3), keepdim=True)
+        g = geo / S
+        if has_gm:
+            g = g + grad_maps.float()
+        gv = g * (v > 0).to(g.dtype)
+    return (gv * mult).to(hm.dtype), None, None, None, None

@@ -97,6 +97,32 @@ def _(vol, coords, softmax, multiplier, return_volume, out_dtype):
     return xyz, vol.new_empty(shape, dtype=_CODE_DTYPE[out_dtype])
 
 
+# --------------------------------------------------------------------------- 2D soft-argmax
+@torch.library.custom_op("mvn_rocm::softargmax2d", mutates_args=())
+def softargmax2d(hm: Tensor, softmax: bool, multiplier: float, return_maps: bool,
+                 out_dtype: int) -> Tuple[Tensor, Tensor]:
+    """hm (B,J,H,W) f32|bf16 contiguous -> (xy (B,J,2) f32, maps (B,J,H,W) or an empty tensor)."""
+    _require_gpu(hm)
+    B, J, H, W = hm.shape
+    xy = torch.empty((B, J, 2), dtype=torch.float32, device=hm.device)
+    if return_maps:
+        maps = torch.empty((B, J, H, W), dtype=_CODE_DTYPE[out_dtype], device=hm.device)
+    else:
+        maps = torch.empty((0,), dtype=_CODE_DTYPE[out_dtype], device=hm.device)
+    code = _lib.load().mvn_softargmax2d(hm.data_ptr(), _DTYPE_CODE[hm.dtype], float(multiplier), int(softmax),
+                                        xy.data_ptr(), maps.data_ptr() if return_maps else None, out_dtype,
+                                        B, J, H, W, _stream(hm))
+    _lib.check(code, "mvn_softargmax2d")
+    return xy, maps
+
+
+@softargmax2d.register_fake
+def _(hm, softmax, multiplier, return_maps, out_dtype):
+    B, J = hm.shape[:2]
+    shape = tuple(hm.shape) if return_maps else (0,)
+    return hm.new_empty((B, J, 2), dtype=torch.float32), hm.new_empty(shape, dtype=_CODE_DTYPE[out_dtype])
+
+
 # --------------------------------------------------------------------------- DLT
 @torch.library.custom_op("mvn_rocm::dlt", mutates_args=())
 def dlt(proj: Tensor, pts: Tensor, conf: Optional[Tensor]) -> Tensor:

@@ -85,6 +85,25 @@ def integrate_tensor_3d_with_coordinates(volumes, coord_volumes, softmax=True, *
     return xyz, (out if return_volumes else None)
 
 
+def integrate_tensor_2d(heatmaps, softmax=True, *, multiplier=1.0, return_heatmaps=True, out_dtype=None):
+    """2D soft-argmax: returns (coordinates (B, J, 2) as (x, y) in pixels, heatmaps (B, J, H, W)).
+
+    Reference: ``mvn/utils/op.py:11-47``.  ``multiplier`` fuses the caller's
+    ``heatmaps * heatmap_multiplier`` (triangulation.py:164).  The returned maps are
+    softmax-normalised, or relu'd and NOT normalised for ``softmax=False`` (op.py:27),
+    whose coordinates are divided by the mass (op.py:40-42).
+    """
+    hm = heatmaps
+    if hm.dtype not in (torch.float32, torch.bfloat16):
+        hm = hm.float()
+    if hm.dim() != 4:
+        raise RuntimeError(f"heatmaps must be (B, J, H, W), got {tuple(hm.shape)}")
+    hm = hm.contiguous()
+    od = _dtype_code(out_dtype if out_dtype is not None else hm.dtype)
+    xy, maps = SoftArgmax2dFunction.apply(hm, bool(softmax), float(multiplier), bool(return_heatmaps), od)
+    return xy, (maps if return_heatmaps else None)
+
+
 class UnprojectFunction(torch.autograd.Function):
     """autograd surface of op.py:99-163; backward: csrc/unproject_bwd.hip (grads w.r.t. the
     features and, for 'conf*', the confidences)."""
@@ -116,3 +135,19 @@ class SoftArgmaxFunction(torch.autograd.Function):
     def backward(ctx, grad_xyz, grad_out):
         from . import _backward
         return _backward.softargmax_backward(ctx, grad_xyz, grad_out)
+
+
+class SoftArgmax2dFunction(torch.autograd.Function):
+    """autograd surface of op.py:11-47; backward in _backward.softargmax2d_backward."""
+
+    @staticmethod
+    def forward(ctx, hm, softmax, multiplier, return_maps, out_dtype):
+        xy, maps = _ops.softargmax2d(hm, softmax, multiplier, return_maps, out_dtype)
+        ctx.save_for_backward(hm, xy)
+        ctx.cfg = (softmax, multiplier)
+        return xy, maps
+
+    @staticmethod
+    def backward(ctx, grad_xy, grad_maps):
+        from . import _backward
+        return _backward.softargmax2d_backward(ctx, grad_xy, grad_maps)

@@ -1,6 +1,7 @@
 """ORACLE — test infrastructure only.
 
-float64 restatement of the confidence-weighted DLT (mvn/utils/multiview.py:132-174).
+float64 restatements: the 2D soft-argmax (mvn/utils/op.py:11-47) and the
+confidence-weighted DLT (mvn/utils/multiview.py:132-174).
 The design matrix is formed in float32 with the reference's three separately rounded
 ops (multiview.py:150-152) and only the null-space solve is promoted to float64
 (LAPACK gesdd via numpy).  This is the gate for the HIP DLT (<= 1e-6 relative): the
@@ -38,3 +39,22 @@ def triangulate_batch_of_points(proj, points, confidences=None) -> np.ndarray:
             X = vh[-1]
             out[b, j] = X[:3] / X[3]
     return out
+
+
+def integrate_tensor_2d(heatmaps, softmax=True):
+    """mvn/utils/op.py:11-47 in float64: (B,J,H,W) -> ((B,J,2) (x, y), normalised maps)."""
+    hm = np.asarray(heatmaps, np.float64)
+    B, J, H, W = hm.shape
+    flat = hm.reshape(B, J, -1)
+    if softmax:
+        e = np.exp(flat - flat.max(axis=2, keepdims=True))
+        p = e / e.sum(axis=2, keepdims=True)
+    else:
+        p = np.maximum(flat, 0.0)
+    p = p.reshape(B, J, H, W)
+    mass = p.sum(axis=(2, 3))
+    x = (p.sum(axis=2) * np.arange(W)).sum(axis=2)
+    y = (p.sum(axis=3) * np.arange(H)).sum(axis=2)
+    if not softmax:
+        x, y = x / mass, y / mass
+    return np.stack([x, y], axis=2), p

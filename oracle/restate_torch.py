@@ -74,6 +74,23 @@ def integrate_tensor_3d_with_coordinates(volumes, coord_volumes, softmax=True):
     return torch.einsum("bnxyz, bxyzc -> bnc", vols, coord_volumes), vols
 
 
+def integrate_tensor_2d(heatmaps, softmax=True):
+    """mvn/utils/op.py:11-47: normalise each flattened map, project its mass onto the two
+    axes, take the first moments (relu mode: divided by the mass)."""
+    n_batch, n_maps, h, w = heatmaps.shape
+    flat = heatmaps.reshape((n_batch, n_maps, -1))
+    flat = F.softmax(flat, dim=2) if softmax else F.relu(flat)
+    maps = flat.reshape((n_batch, n_maps, h, w))
+    col_mass = maps.sum(dim=2)                      # over rows -> mass per column (x)
+    row_mass = maps.sum(dim=3)                      # over columns -> mass per row (y)
+    x = (col_mass * torch.arange(w).type(torch.float).to(maps.device)).sum(dim=2, keepdim=True)
+    y = (row_mass * torch.arange(h).type(torch.float).to(maps.device)).sum(dim=2, keepdim=True)
+    if not softmax:
+        x = x / col_mass.sum(dim=2, keepdim=True)
+        y = y / row_mass.sum(dim=2, keepdim=True)
+    return torch.cat((x, y), dim=2).reshape((n_batch, n_maps, 2)), maps
+
+
 def triangulate_batch_of_points(proj_matricies_batch, points_batch, confidences_batch=None):
     """mvn/utils/multiview.py:162-174 with the solver of :132-159 inlined."""
     n_batch, n_views, n_joints = points_batch.shape[:3]

@@ -2,7 +2,7 @@
 
 Run in the build container only (it needs /root/reference; the GPU box never runs it):
 
-    python -B tests/golden/make_golden.py
+    python -B tests/golden/make_golden.py [softargmax2d]      (argument: only that fixture)
 
 The reference (learnable-triangulation-pytorch, mvn/utils/op.py and
 mvn/utils/multiview.py) is imported read-only with two in-memory accommodations:
@@ -111,8 +111,41 @@ def small_unproject_inputs(seed=0):
     return feat, proj.astype(np.float32), coords, conf
 
 
+def golden_softargmax2d(op):
+    """integrate_tensor_2d (op.py:11-47): small non-square maps, softmax / relu, the
+    caller's heatmap_multiplier (triangulation.py:164), gradients; and a config-shaped
+    slice (4 views x 17 joints of 96^2 blob heatmaps)."""
+    rng = np.random.default_rng(21)
+    hm = (rng.standard_normal((2, 5, 17, 23)) * 3.0).astype(np.float32)
+    sa = {}
+    for softmax in (True, False):
+        for mult in (1.0, 1.7):
+            h = torch.from_numpy(hm).requires_grad_(True)
+            xy, maps = op.integrate_tensor_2d(h * mult, softmax)
+            key = f"sm{int(softmax)}_m{mult}"
+            sa[f"xy_{key}"] = xy.detach().numpy()
+            sa[f"maps_{key}"] = maps.detach().numpy()
+            gxy = torch.from_numpy(rng.standard_normal(xy.shape).astype(np.float32))
+            gm = torch.from_numpy((rng.standard_normal(maps.shape) * 1e-2).astype(np.float32))
+            torch.autograd.backward([xy, maps], [gxy, gm])
+            sa[f"grad_xy_{key}"] = gxy.numpy()
+            sa[f"grad_maps_{key}"] = gm.numpy()
+            sa[f"grad_in_{key}"] = h.grad.numpy()
+    # config-shaped: (B*N, J, 96, 96) Gaussian blobs at random centres
+    H = W = 96
+    yy, xx = np.mgrid[0:H, 0:W]
+    cx, cy = rng.uniform(5, W - 5, (4, 17)), rng.uniform(5, H - 5, (4, 17))
+    blob = np.exp(-((xx - cx[..., None, None]) ** 2 + (yy - cy[..., None, None]) ** 2) / (2 * 2.0 ** 2))
+    cfg = (blob * 10.0).astype(np.float32)
+    xy, _ = op.integrate_tensor_2d(torch.from_numpy(cfg) * 1.0, True)
+    save("softargmax2d.npz", hm=hm, cfg=cfg, cfg_xy=xy.numpy(), **sa)
+
+
 def main():
     op, multiview = import_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "softargmax2d":
+        golden_softargmax2d(op)
+        return
     torch.manual_seed(0)
 
     # --- unproject: small, every aggregation, both align_corners, f32 and bf16-rounded input
@@ -204,6 +237,8 @@ def main():
         dl[f"conf_{name}"] = ab.confidences.numpy()
         dl[f"gt_{name}"] = ab.points_3d.numpy()
     save("dlt.npz", **dl)
+
+    golden_softargmax2d(op)
 
 
 if __name__ == "__main__":

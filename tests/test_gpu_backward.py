@@ -97,3 +97,15 @@ def test_dlt_backward(golden, device, case, use_conf):
     if use_conf:
         assert max_rel(conf.grad.cpu().numpy(), c64.grad.numpy()) <= 1e-5
         assert max_rel(conf.grad.cpu().numpy(), d[f"grad_conf_{key}"]) <= 5e-2
+
+
+@pytest.mark.parametrize("softmax", (True, False))
+@pytest.mark.parametrize("mult", (1.0, 1.7))
+def test_softargmax2d_backward_matches_reference_autograd(golden, device, softmax, mult):
+    from mvn_rocm import op
+    d = golden("softargmax2d.npz")
+    key = f"sm{int(softmax)}_m{mult}"
+    h = _t(d["hm"], device).requires_grad_(True)
+    xy, maps = op.integrate_tensor_2d(h, softmax, multiplier=mult)
+    torch.autograd.backward([xy, maps], [_t(d[f"grad_xy_{key}"], device), _t(d[f"grad_maps_{key}"], device)])
+    assert max_rel(h.grad.cpu().numpy(), d[f"grad_in_{key}"]) <= 1e-5

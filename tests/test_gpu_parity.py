@@ -297,3 +297,29 @@ def test_hip_library_is_the_one_loaded():
     _lib.load()
     maps = open("/proc/self/maps").read()
     assert _lib.LIB_PATH in maps
+
+
+# ----------------------------------------------------------------------------- 2D soft-argmax
+@pytest.mark.parametrize("softmax", (True, False))
+@pytest.mark.parametrize("mult", (1.0, 1.7))
+def test_softargmax2d_matches_reference_golden(golden, device, softmax, mult):
+    d = golden("softargmax2d.npz")
+    key = f"sm{int(softmax)}_m{mult}"
+    xy, maps = _op().integrate_tensor_2d(_t(d["hm"], device), softmax, multiplier=mult)
+    assert xy.shape == (2, 5, 2) and maps.shape == (2, 5, 17, 23)
+    assert max_rel(xy.cpu().numpy(), d[f"xy_{key}"]) <= 1e-5
+    assert max_rel(maps.cpu().numpy(), d[f"maps_{key}"]) <= 1e-5
+
+
+def test_softargmax2d_cfg_slice_and_bf16(golden, device):
+    d = golden("softargmax2d.npz")
+    xy, _ = _op().integrate_tensor_2d(_t(d["cfg"], device), return_heatmaps=False)
+    ref64, _ = restate_np.integrate_tensor_2d(d["cfg"], True)
+    assert max_rel(xy.cpu().numpy(), ref64) <= 1e-5
+    assert max_rel(xy.cpu().numpy(), d["cfg_xy"]) <= 5e-5     # the f32 reference is 1.2e-5 off f64
+    h16 = _t(d["hm"], device).to(torch.bfloat16)
+    ref_xy, ref_maps = restate_np.integrate_tensor_2d(h16.float().cpu().numpy() * 1.7, True)
+    xy, maps = _op().integrate_tensor_2d(h16, multiplier=1.7)
+    assert maps.dtype == torch.bfloat16
+    assert max_rel(xy.cpu().numpy(), ref_xy) <= 1e-5
+    np.testing.assert_allclose(maps.float().cpu().numpy(), ref_maps, rtol=2 ** -8, atol=1e-30)

@@ -118,3 +118,29 @@ def test_dlt_oracles(golden, case, use_conf):
             a_n = restate_np.design_matrix(d[f"proj_{case}"][b], d[f"points_{case}"][b, :, j],
                                            None if conf is None else conf[b, :, j])
             np.testing.assert_array_equal(a_c, a_n)
+
+
+@pytest.mark.parametrize("softmax", (True, False))
+@pytest.mark.parametrize("mult", (1.0, 1.7))
+def test_softargmax2d_oracles(golden, softmax, mult):
+    """integrate_tensor_2d (op.py:11-47): the torch restatement reproduces the reference's
+    bits; the float64 restatement is within f32 rounding."""
+    d = golden("softargmax2d.npz")
+    key = f"sm{int(softmax)}_m{mult}"
+    h = torch.from_numpy(d["hm"]) * mult
+    xy, maps = restate_torch.integrate_tensor_2d(h, softmax)
+    np.testing.assert_array_equal(xy.numpy(), d[f"xy_{key}"])
+    np.testing.assert_array_equal(maps.numpy(), d[f"maps_{key}"])
+    xy64, maps64 = restate_np.integrate_tensor_2d(h.numpy(), softmax)
+    assert max_rel(xy64, d[f"xy_{key}"]) <= 1e-6
+    assert max_rel(maps64, d[f"maps_{key}"]) <= 1e-6
+
+
+def test_softargmax2d_oracle_cfg_slice(golden):
+    """96^2 peaked maps: the f32 reference's own summation error (9216-term mass sums times
+    the pixel index) is 1.2e-5 relative to the float64 restatement — inside the 1e-4 bar."""
+    d = golden("softargmax2d.npz")
+    xy64, _ = restate_np.integrate_tensor_2d(d["cfg"], True)
+    assert max_rel(xy64, d["cfg_xy"]) <= 5e-5
+    xy, _ = restate_torch.integrate_tensor_2d(torch.from_numpy(d["cfg"]), True)
+    np.testing.assert_array_equal(xy.numpy(), d["cfg_xy"])

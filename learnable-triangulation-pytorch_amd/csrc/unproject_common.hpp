@@ -47,6 +47,70 @@ __device__ __forceinline__ Proj project(const float* __restrict__ Pv, float x, f
   return p;
 }
 
+// ---- projection with a cheaper exact division (the tiled kernel's prologue) --------
+// f32 '/' is compiled to v_div_scale x2, v_rcp, 5 fma/mul, v_div_fmas, v_div_fixup.  When
+// no range scaling is needed (v_div_scale leaves both operands alone and VCC clear),
+// v_div_fmas is a plain fma and v_div_fixup returns its input for finite normal results,
+// so the remaining refinement chain below is bit-identical to '/'.  div_core_safe()
+// bounds the operands so that this holds (|d| in [2^-30, 2^30], |n| <= 2^60: exponent
+// difference < 96, no denormal reciprocal; a tiny |n| can only yield a tiny quotient,
+// which the following `2 * (q / size - 0.5)` absorbs identically in both forms).
+struct Recip {
+  float d, r;   // denominator and its once-refined reciprocal (the compiler's fma0/fma1)
+};
+__device__ __forceinline__ Recip recip_refined(float d) {
+  const float r0 = __builtin_amdgcn_rcpf(d);
+  const float e = __builtin_fmaf(-d, r0, 1.f);
+  return Recip{d, __builtin_fmaf(e, r0, r0)};
+}
+__device__ __forceinline__ float div_core(float n, Recip q) {
+  const float q0 = n * q.r;
+  const float t0 = __builtin_fmaf(-q.d, q0, n);
+  const float q1 = __builtin_fmaf(t0, q.r, q0);
+  const float t1 = __builtin_fmaf(-q.d, q1, n);
+  return __builtin_fmaf(t1, q.r, q1);
+}
+
+struct Homog {
+  float uh, vh, wh;   // [x y z 1] @ P^T (op.py:117-119 -> multiview.py:96)
+};
+__device__ __forceinline__ Homog homog(const float* __restrict__ Pv, float x, float y, float z) {
+  Homog h;
+  h.uh = __builtin_fmaf(1.f, Pv[3], __builtin_fmaf(z, Pv[2], __builtin_fmaf(y, Pv[1], x * Pv[0])));
+  h.vh = __builtin_fmaf(1.f, Pv[7], __builtin_fmaf(z, Pv[6], __builtin_fmaf(y, Pv[5], x * Pv[4])));
+  h.wh = __builtin_fmaf(1.f, Pv[11], __builtin_fmaf(z, Pv[10], __builtin_fmaf(y, Pv[9], x * Pv[8])));
+  return h;
+}
+__device__ __forceinline__ bool div_core_safe(const Homog& h) {
+  const float aw = fabsf(h.wh == 0.f ? 1.f : h.wh);
+  return aw >= 0x1p-30f && aw <= 0x1p30f && fabsf(h.uh) <= 0x1p60f && fabsf(h.vh) <= 0x1p60f;
+}
+// project() from a homogeneous point; FAST: div_core (caller checked div_core_safe on the
+// whole wave), else IEEE '/'.  Same op order as project().
+template <bool FAST>
+__device__ __forceinline__ Proj project_h(const Homog& hp, int H, int W, int align_corners, Recip rH, Recip rW) {
+  Proj p;
+  p.invalid = hp.wh <= 0.f;                // op.py:121
+  const float wh = hp.wh == 0.f ? 1.f : hp.wh;
+  float gx, gy;
+  if constexpr (FAST) {
+    const Recip rw = recip_refined(wh);
+    gx = 2.f * (div_core(div_core(hp.uh, rw), rH) - 0.5f);
+    gy = 2.f * (div_core(div_core(hp.vh, rw), rW) - 0.5f);
+  } else {
+    gx = 2.f * ((hp.uh / wh) / float(H) - 0.5f);
+    gy = 2.f * ((hp.vh / wh) / float(W) - 0.5f);
+  }
+  if (align_corners) {
+    p.ix = (gx + 1.f) * (float(W - 1) * 0.5f);
+    p.iy = (gy + 1.f) * (float(H - 1) * 0.5f);
+  } else {
+    p.ix = __builtin_fmaf(gx + 1.f, float(W) * 0.5f, -0.5f);
+    p.iy = __builtin_fmaf(gy + 1.f, float(H) * 0.5f, -0.5f);
+  }
+  return p;
+}
+
 __device__ __forceinline__ Taps view_taps(const float* __restrict__ Pv, float x, float y, float z,
                                           int H, int W, int align_corners) {
   const Proj p = project(Pv, x, y, z, H, W, align_corners);

@@ -253,13 +253,22 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
   int fx[NV], fy[NV];
   float w[NV][4];
   bool has[NV];
+  bool lane_fast = true;
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    if (v < N) lane_fast &= div_core_safe(homog(Pb + v * 12, cx, cy, cz));
+  // wave-uniform choice of the division form (bit-identical results either way)
+  const bool wave_fast = __builtin_amdgcn_ballot_w64(!lane_fast) == 0;
+  const Recip rH = recip_refined(float(H)), rW = recip_refined(float(W));
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     has[v] = false;
     fx[v] = fy[v] = 0;
     w[v][0] = w[v][1] = w[v][2] = w[v][3] = 0.f;
     if (v < N) {
-      const Proj p = project(Pb + v * 12, cx, cy, cz, H, W, align_corners);
+      const Homog hp = homog(Pb + v * 12, cx, cy, cz);
+      const Proj p = (EXACT && wave_fast) ? project_h<true>(hp, H, W, align_corners, rH, rW)
+                                          : project_h<false>(hp, H, W, align_corners, rH, rW);
       const float fx0 = floorf(p.ix), fy0 = floorf(p.iy);
       // at least one of the 4 taps lies inside the image, and the voxel is in front
       const bool h = act & !p.invalid & (fx0 >= -1.f) & (fx0 < float(W)) & (fy0 >= -1.f) & (fy0 < float(H));

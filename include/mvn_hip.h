@@ -13,6 +13,8 @@
  *                           (+ its per-point solver multiview.py:132-159)
  *   mvn_softargmax2d     <- mvn/utils/op.py:11-47    integrate_tensor_2d(...)  (the algebraic
  *                           path's producer of the DLT's 2D points)
+ *   mvn_coord_volumes    <- mvn/models/triangulation.py:280-341 (the per-frame coordinate-
+ *                           volume loop feeding unproject and soft-argmax)
  *
  * Conventions
  *   - Every buffer is caller-owned device memory (hipMalloc / torch), contiguous,
@@ -128,6 +130,16 @@ int mvn_dlt(const float* proj, const float* pts, const float* conf, float* out,
  */
 int mvn_softargmax2d(const void* heatmaps, int dtype, float multiplier, int softmax, float* out_xy,
                      void* out_maps, int out_dtype, int B, int J, int H, int W, void* stream);
+
+/*
+ * Coordinate volumes (B, V, V, V, 3) f32 of the volumetric model, replacing the per-frame
+ * loop of triangulation.py:280-341 (cuboid grid, rotation about the base point,
+ * volumetric.py:87-114, optional CMU -> Human3.6M re-axing).  The caller forms per frame,
+ * in float64 and rounded to f32 as torch does: position (B,3) = base - side/2,
+ * centre (B,3) = base point, step (B,3) = side / (V-1), rot (B,3,3) the rotation matrix.
+ */
+int mvn_coord_volumes(const float* position, const float* centre, const float* step, const float* rot,
+                      float* out, int B, int V, int transfer_cmu, void* stream);
 
 /* ---- backward (autograd) ------------------------------------------------------------
  * Gradients of the three ops, replacing the ATen autograd the reference relies on

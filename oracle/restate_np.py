@@ -58,3 +58,39 @@ def integrate_tensor_2d(heatmaps, softmax=True):
     if not softmax:
         x, y = x / mass, y / mass
     return np.stack([x, y], axis=2), p
+
+
+def coord_volumes(base_points, cuboid_side, volume_size, thetas, kind="coco", transfer_cmu=False):
+    """mvn/models/triangulation.py:280-341 in numpy, reproducing the reference's f32 bits
+    as the reference computes them on this container's CPU (MKL's K=3 sgemm accumulates
+    rot.mm as an fma chain over k = 0, 1, 2; verified against tests/golden/coord_volumes.npz,
+    which ran the reference's own rotate_coord_volume).  Host-independent, unlike a torch
+    re-run, whose sgemm order follows the host's MKL code path."""
+    f = np.float32
+
+    def fma(a, b, c):
+        return (np.float64(a) * np.float64(b) + np.float64(c)).astype(f)
+
+    base_points = np.asarray(base_points, np.float64)
+    V = int(volume_size)
+    out = np.zeros((len(base_points), V, V, V, 3), f)
+    i, j, k = np.meshgrid(np.arange(V), np.arange(V), np.arange(V), indexing="ij")
+    g = (i, k, V - 1 - j) if transfer_cmu else (i, j, k)
+    axis = np.array([0, 1, 0] if kind == "coco" else [0, 0, 1], np.float64)
+    axis = axis / np.sqrt(np.dot(axis, axis))
+    for b, base in enumerate(base_points):
+        pos = (base - cuboid_side / 2.0).astype(f)
+        st = f(cuboid_side / (V - 1))
+        cen = base.astype(f)
+        th = float(np.asarray(thetas, np.float64).reshape(-1)[b] if np.ndim(thetas) else thetas)
+        a = np.cos(th / 2.0)
+        bq, cq, dq = -axis * np.sin(th / 2.0)
+        aa, bb, cc, dd = a * a, bq * bq, cq * cq, dq * dq
+        bc, ad, ac, ab, bd, cd = bq * cq, a * dq, a * cq, a * bq, bq * dq, cq * dq
+        R = np.array([[aa + bb - cc - dd, 2 * (bc + ad), 2 * (bd - ac)],
+                      [2 * (bc - ad), aa + cc - bb - dd, 2 * (cd + ab)],
+                      [2 * (bd + ac), 2 * (cd - ab), aa + dd - bb - cc]]).astype(f)
+        d = [((pos[q] + (st * g[q].astype(f)).astype(f)).astype(f) - cen[q]).astype(f) for q in range(3)]
+        out[b] = np.stack([(fma(R[r, 2], d[2], fma(R[r, 1], d[1], (R[r, 0] * d[0]).astype(f))) + cen[r]).astype(f)
+                           for r in range(3)], -1)
+    return out

@@ -110,3 +110,50 @@ def triangulate_batch_of_points(proj_matricies_batch, points_batch, confidences_
             X = -V[:, 3]                                                        # :156
             out[b, j] = _from_homogeneous(X.unsqueeze(0))[0]                    # :157
     return out
+
+
+def build_coord_volumes(base_points, cuboid_side, volume_size, thetas, kind="coco", transfer_cmu=False,
+                        rotate=None):
+    """mvn/models/triangulation.py:280-341, the per-frame loop, op for op (torch CPU).
+    ``rotate`` defaults to this module's restatement of volumetric.rotate_coord_volume
+    (volumetric.py:103-114); the golden script passes the reference's own function."""
+    import numpy as np
+    rotate = rotate or rotate_coord_volume
+    V = volume_size
+    out = torch.zeros(len(base_points), V, V, V, 3)
+    for b, base_point in enumerate(np.asarray(base_points, dtype=np.float64)):
+        sides = np.array([cuboid_side, cuboid_side, cuboid_side])
+        position = base_point - sides / 2
+        xxx, yyy, zzz = torch.meshgrid(torch.arange(V), torch.arange(V), torch.arange(V), indexing="ij")
+        grid = torch.stack([xxx, yyy, zzz], dim=-1).type(torch.float).reshape((-1, 3))
+        grid_coord = torch.zeros_like(grid)
+        for k in range(3):
+            grid_coord[:, k] = position[k] + (sides[k] / (V - 1)) * grid[:, k]
+        coord_volume = grid_coord.reshape(V, V, V, 3)
+        axis = [0, 1, 0] if kind == "coco" else [0, 0, 1]
+        center = torch.from_numpy(base_point).type(torch.float)
+        coord_volume = coord_volume - center
+        coord_volume = rotate(coord_volume, float(thetas[b]), axis)
+        coord_volume = coord_volume + center
+        if transfer_cmu:
+            coord_volume = coord_volume.permute(0, 2, 1, 3)
+            coord_volume = coord_volume.index_select(1, torch.arange(V - 1, -1, -1).long())
+        out[b] = coord_volume
+    return out
+
+
+def rotate_coord_volume(coord_volume, theta, axis):
+    """volumetric.py:103-114 (rotation matrix of :87-100 in float64, cast to f32, sgemm)."""
+    import numpy as np
+    axis = np.asarray(axis, dtype=np.float64)
+    axis = axis / np.sqrt(np.dot(axis, axis))
+    a = np.cos(theta / 2.0)
+    b, c, d = -axis * np.sin(theta / 2.0)
+    aa, bb, cc, dd = a * a, b * b, c * c, d * d
+    bc, ad, ac, ab, bd, cd = b * c, a * d, a * c, a * b, b * d, c * d
+    rot = np.array([[aa + bb - cc - dd, 2 * (bc + ad), 2 * (bd - ac)],
+                    [2 * (bc - ad), aa + cc - bb - dd, 2 * (cd + ab)],
+                    [2 * (bd + ac), 2 * (cd - ab), aa + dd - bb - cc]])
+    rot = torch.from_numpy(rot).type(torch.float)
+    shape = coord_volume.shape
+    return rot.mm(coord_volume.reshape(-1, 3).t()).t().reshape(*shape)

@@ -2,7 +2,7 @@
 
 Run in the build container only (it needs /root/reference; the GPU box never runs it):
 
-    python -B tests/golden/make_golden.py [softargmax2d]      (argument: only that fixture)
+    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes]   (argument: only that fixture)
 
 The reference (learnable-triangulation-pytorch, mvn/utils/op.py and
 mvn/utils/multiview.py) is imported read-only with two in-memory accommodations:
@@ -141,10 +141,33 @@ def golden_softargmax2d(op):
     save("softargmax2d.npz", hm=hm, cfg=cfg, cfg_xy=xy.numpy(), **sa)
 
 
+def golden_coord_volumes():
+    """Coordinate volumes of triangulation.py:280-341.  The grid/centring is the loop's
+    own ATen op sequence (restated in oracle/restate_torch.py: that code is inline in the
+    model's forward, not a function); the rotation is the reference's own
+    volumetric.rotate_coord_volume (volumetric.py:103-114), called here."""
+    from mvn.utils import volumetric  # noqa: WPS433 (reference, imported above)
+    sys.path.insert(0, REPO)
+    from oracle import restate_torch
+    rng = np.random.default_rng(33)
+    base = np.stack([rng.uniform(-500, 500, 3) + np.array([0, 0, 900.0]) for _ in range(3)])
+    cases = {"coco_eval": ("coco", [0.0, 0.0, 0.0], False), "coco_train": ("coco", [1.234, 4.5, 0.3], False),
+             "mpii_cmu": ("mpii", [0.7, 2.2, 5.9], True)}
+    out = {"base": base}
+    for name, (kind, thetas, cmu) in cases.items():
+        cv = restate_torch.build_coord_volumes(base, 2500.0, 16, thetas, kind, cmu, rotate=volumetric.rotate_coord_volume)
+        out[f"cv_{name}"] = cv.numpy()
+        out[f"theta_{name}"] = np.asarray(thetas)
+    save("coord_volumes.npz", **out)
+
+
 def main():
     op, multiview = import_reference()
     if len(sys.argv) > 1 and sys.argv[1] == "softargmax2d":
         golden_softargmax2d(op)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "coord_volumes":
+        golden_coord_volumes()
         return
     torch.manual_seed(0)
 
@@ -239,6 +262,7 @@ def main():
     save("dlt.npz", **dl)
 
     golden_softargmax2d(op)
+    golden_coord_volumes()
 
 
 if __name__ == "__main__":

@@ -323,3 +323,24 @@ def test_softargmax2d_cfg_slice_and_bf16(golden, device):
     assert maps.dtype == torch.bfloat16
     assert max_rel(xy.cpu().numpy(), ref_xy) <= 1e-5
     np.testing.assert_allclose(maps.float().cpu().numpy(), ref_maps, rtol=2 ** -8, atol=1e-30)
+
+
+# ----------------------------------------------------------------------------- coordinate volumes
+@pytest.mark.parametrize("case", ("coco_eval", "coco_train", "mpii_cmu"))
+def test_coord_volumes_match_reference_golden(golden, device, case):
+    from mvn_rocm import volumetric
+    d = golden("coord_volumes.npz")
+    kind = "coco" if case.startswith("coco") else "mpii"
+    cv = volumetric.build_coord_volumes(d["base"], 2500.0, 16, d[f"theta_{case}"], kind, case == "mpii_cmu",
+                                        device=device)
+    np.testing.assert_array_equal(cv.cpu().numpy(), d[f"cv_{case}"])
+
+
+def test_coord_volumes_full_size_vs_restatement(device):
+    from mvn_rocm import volumetric
+    rng = np.random.default_rng(5)
+    base = rng.uniform(-500, 500, (2, 3)) + np.array([0, 0, 900.0])
+    thetas = rng.uniform(0, 2 * np.pi, 2)
+    ref = restate_np.coord_volumes(base, 2500.0, 64, thetas, "coco", False)   # pinned by the goldens
+    cv = volumetric.build_coord_volumes(base, 2500.0, 64, thetas, "coco", False, device=device)
+    np.testing.assert_array_equal(cv.cpu().numpy(), ref)

@@ -144,3 +144,22 @@ def test_softargmax2d_oracle_cfg_slice(golden):
     assert max_rel(xy64, d["cfg_xy"]) <= 5e-5
     xy, _ = restate_torch.integrate_tensor_2d(torch.from_numpy(d["cfg"]), True)
     np.testing.assert_array_equal(xy.numpy(), d["cfg_xy"])
+
+
+@pytest.mark.parametrize("case", ("coco_eval", "coco_train", "mpii_cmu"))
+def test_coord_volume_restatement(golden, case):
+    """triangulation.py:280-341 restated op for op, with its own rotation restatement, equals
+    the loop run through the reference's volumetric.rotate_coord_volume bit for bit."""
+    d = golden("coord_volumes.npz")
+    kind = "coco" if case.startswith("coco") else "mpii"
+    cv = restate_torch.build_coord_volumes(d["base"], 2500.0, 16, d[f"theta_{case}"], kind, case == "mpii_cmu")
+    np.testing.assert_array_equal(cv.numpy(), d[f"cv_{case}"])
+
+
+def test_coord_volume_numpy_recipe(golden):
+    """The kernel's f32 op order (csrc/coord_volumes.hip), restated in numpy
+    (oracle/restate_np.coord_volumes), reproduces the reference's bits."""
+    d = golden("coord_volumes.npz")
+    for case, kind, cmu in (("coco_eval", "coco", False), ("coco_train", "coco", False), ("mpii_cmu", "mpii", True)):
+        cv = restate_np.coord_volumes(d["base"], 2500.0, 16, d[f"theta_{case}"], kind, cmu)
+        np.testing.assert_array_equal(cv, d[f"cv_{case}"])

@@ -15,6 +15,8 @@
  *                           path's producer of the DLT's 2D points)
  *   mvn_coord_volumes    <- mvn/models/triangulation.py:280-341 (the per-frame coordinate-
  *                           volume loop feeding unproject and soft-argmax)
+ *   mvn_nearest_voxel    <- mvn/models/loss.py:63-67 (VolumetricCELoss's distance volume +
+ *                           argmin)
  *
  * Conventions
  *   - Every buffer is caller-owned device memory (hipMalloc / torch), contiguous,
@@ -140,6 +142,14 @@ int mvn_softargmax2d(const void* heatmaps, int dtype, float multiplier, int soft
  */
 int mvn_coord_volumes(const float* position, const float* centre, const float* step, const float* rot,
                       float* out, int B, int V, int transfer_cmu, void* stream);
+
+/*
+ * Nearest voxel per (frame, joint): argmin over the V^3 voxels of the f32 squared distance
+ * between coords[b] (B, Vx, Vy, Vz, 3) and keypoints (B, J, 3); first index on ties.
+ *   out_index (B, J) int32, flat row-major voxel index (VolumetricCELoss, loss.py:63-67).
+ */
+int mvn_nearest_voxel(const float* coords, const float* keypoints, int* out_index, int B, int J,
+                      int Vx, int Vy, int Vz, void* stream);
 
 /* ---- backward (autograd) ------------------------------------------------------------
  * Gradients of the three ops, replacing the ATen autograd the reference relies on

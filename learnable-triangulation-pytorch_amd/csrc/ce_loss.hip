@@ -1,0 +1,65 @@
+// Nearest-voxel search of the volumetric cross-entropy loss for gfx950 (SURVEY.md §8f
+// rank 4).
+//
+// Replaces the distance volume + torch.argmin of mvn/models/loss.py:63-67
+// (VolumetricCELoss): for every (frame, joint) the index of the voxel whose coordinate is
+// closest to the ground-truth keypoint.  The reference takes the argmin of
+// sqrt(sum((c - k)^2)) with the sum in sequence over x, y, z (f32, verified) and the
+// FIRST minimal index; here the argmin of the same f32 squared sum, first index on ties.
+// sqrt is monotonic, so the two agree except where the reference's rounded square roots
+// tie two distinct squared distances (the nearest voxel is ~1 voxel pitch closer than the
+// next, so this does not occur on real grids; tests check the golden's gradients, which
+// are non-zero exactly at the reference's argmin voxels).
+// One 256-thread block per (frame, joint); the coordinate volume is read once per joint
+// (L2-resident across the joints of a frame).  Output: int32 flat voxel index.
+#include <climits>
+
+#include "common.hpp"
+
+namespace mvn {
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ void better(float& d, int& i, float d2, int i2) {
+  if (d2 < d || (d2 == d && i2 < i)) { d = d2; i = i2; }
+}
+
+__global__ __launch_bounds__(kBlock) void nearest_voxel(const float* __restrict__ coords, const float* __restrict__ kps,
+                                                       int* __restrict__ out, int J, int nvox) {
+  __shared__ float sd[kBlock / kWave];
+  __shared__ int si[kBlock / kWave];
+  const int bj = blockIdx.x, b = bj / J;
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const float kx = kps[bj * 3], ky = kps[bj * 3 + 1], kz = kps[bj * 3 + 2];
+  const float* c = coords + size_t(b) * nvox * 3;
+  float best = INFINITY;
+  int bi = INT_MAX;
+  for (int i = t; i < nvox; i += kBlock) {
+    const float dx = c[size_t(i) * 3] - kx, dy = c[size_t(i) * 3 + 1] - ky, dz = c[size_t(i) * 3 + 2] - kz;
+    const float d = (dx * dx + dy * dy) + dz * dz;   // loss.py:63, summed x, y, z in order
+    better(best, bi, d, i);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) better(best, bi, __shfl_xor(best, o, kWave), __shfl_xor(bi, o, kWave));
+  if (lane == 0) { sd[wid] = best; si[wid] = bi; }
+  __syncthreads();
+  if (t == 0) {
+    for (int w = 1; w < kBlock / kWave; ++w) better(best, bi, sd[w], si[w]);
+    out[bj] = (bi == INT_MAX) ? 0 : bi;             // all-NaN distances: voxel 0 (torch: NaN's index)
+  }
+}
+
+}  // namespace
+}  // namespace mvn
+
+extern "C" int mvn_nearest_voxel(const float* coords, const float* keypoints, int* out_index, int B, int J,
+                                 int Vx, int Vy, int Vz, void* stream) {
+  using namespace mvn;
+  if (!coords || !keypoints || !out_index) return MVN_ERR_ARG;
+  if (B <= 0 || J <= 0 || Vx <= 0 || Vy <= 0 || Vz <= 0) return MVN_ERR_SHAPE;
+  const long long nvox = (long long)Vx * Vy * Vz;
+  if (nvox > (1LL << 30) || (long long)B * J > (1LL << 31) - 1) return MVN_ERR_SHAPE;
+  nearest_voxel<<<B * J, kBlock, 0, static_cast<hipStream_t>(stream)>>>(coords, keypoints, out_index, J, int(nvox));
+  return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
+}

@@ -157,3 +157,19 @@ def rotate_coord_volume(coord_volume, theta, axis):
     rot = torch.from_numpy(rot).type(torch.float)
     shape = coord_volume.shape
     return rot.mm(coord_volume.reshape(-1, 3).t()).t().reshape(*shape)
+
+
+def volumetric_ce_loss(coord_volumes_batch, volumes_batch_pred, keypoints_gt, keypoints_binary_validity):
+    """mvn/models/loss.py:55-80: per frame a (J, V^3) distance volume, its argmin per joint,
+    and the validity-weighted -log of the predicted probability there, summed in order."""
+    import numpy as np
+    loss, n_losses = 0.0, 0
+    for b in range(volumes_batch_pred.shape[0]):
+        dists = torch.sqrt(((coord_volumes_batch[b].unsqueeze(0)
+                             - keypoints_gt[b].unsqueeze(1).unsqueeze(1).unsqueeze(1)) ** 2).sum(-1))
+        idx = torch.argmin(dists.view(dists.shape[0], -1), dim=-1).detach().cpu().numpy()
+        idx = np.stack(np.unravel_index(idx, volumes_batch_pred.shape[-3:]), axis=1)
+        for j, (x, y, z) in enumerate(idx):
+            loss += keypoints_binary_validity[b, j][0] * (-torch.log(volumes_batch_pred[b, j, x, y, z] + 1e-6))
+            n_losses += 1
+    return loss / n_losses

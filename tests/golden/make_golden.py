@@ -2,7 +2,7 @@
 
 Run in the build container only (it needs /root/reference; the GPU box never runs it):
 
-    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes]   (argument: only that fixture)
+    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes|ce_loss]   (argument: only that fixture)
 
 The reference (learnable-triangulation-pytorch, mvn/utils/op.py and
 mvn/utils/multiview.py) is imported read-only with two in-memory accommodations:
@@ -161,8 +161,28 @@ def golden_coord_volumes():
     save("coord_volumes.npz", **out)
 
 
+def golden_ce_loss():
+    """VolumetricCELoss (loss.py:52-80): loss value and d loss / d volumes, which is
+    non-zero exactly at the reference's argmin voxels (so it pins them)."""
+    from mvn.models.loss import VolumetricCELoss  # noqa: WPS433 (reference)
+    vb = synth.volumetric_batch(2, n_views=4, channels=1, volume=16, seed=17)
+    rng = np.random.default_rng(17)
+    kps = (vb.coords.reshape(2, -1, 3)[:, rng.integers(0, 16 ** 3, 17)].numpy()
+           + rng.normal(0, 30.0, (2, 17, 3))).astype(np.float32)
+    logits = torch.from_numpy(rng.standard_normal((2, 17, 16 ** 3)).astype(np.float32) * 3)
+    vol = torch.softmax(logits, dim=2).reshape(2, 17, 16, 16, 16).contiguous().requires_grad_(True)
+    validity = (rng.uniform(size=(2, 17, 1)) > 0.2).astype(np.float32)
+    loss = VolumetricCELoss()(vb.coords, vol, torch.from_numpy(kps), torch.from_numpy(validity))
+    loss.backward()
+    save("ce_loss.npz", coords=vb.coords.numpy(), vol=vol.detach().numpy(), kps=kps, validity=validity,
+         loss=loss.detach().numpy(), grad_vol=vol.grad.numpy())
+
+
 def main():
     op, multiview = import_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "ce_loss":
+        golden_ce_loss()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "softargmax2d":
         golden_softargmax2d(op)
         return
@@ -263,6 +283,7 @@ def main():
 
     golden_softargmax2d(op)
     golden_coord_volumes()
+    golden_ce_loss()
 
 
 if __name__ == "__main__":

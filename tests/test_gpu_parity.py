@@ -344,3 +344,25 @@ def test_coord_volumes_full_size_vs_restatement(device):
     ref = restate_np.coord_volumes(base, 2500.0, 64, thetas, "coco", False)   # pinned by the goldens
     cv = volumetric.build_coord_volumes(base, 2500.0, 64, thetas, "coco", False, device=device)
     np.testing.assert_array_equal(cv.cpu().numpy(), ref)
+
+
+# ----------------------------------------------------------------------------- VolumetricCELoss
+def test_nearest_voxel_and_ce_loss_match_reference(golden, device):
+    from mvn_rocm import loss as mloss
+    d = golden("ce_loss.npz")
+    idx = mloss.nearest_voxel(_t(d["coords"], device), _t(d["kps"], device))
+    np.testing.assert_array_equal(idx.cpu().numpy(), restate_np.nearest_voxel(d["coords"], d["kps"]))
+    vol = _t(d["vol"], device).requires_grad_(True)
+    loss = mloss.VolumetricCELoss()(_t(d["coords"], device), vol, _t(d["kps"], device), _t(d["validity"], device))
+    loss.backward()
+    assert abs(float(loss) - float(d["loss"])) <= 1e-6 * abs(float(d["loss"]))
+    assert max_rel(vol.grad.cpu().numpy(), d["grad_vol"]) <= 1e-6
+
+
+def test_nearest_voxel_full_size(device):
+    from mvn_rocm import loss as mloss, synth
+    vb = synth.volumetric_batch(2, channels=1, seed=4)
+    rng = np.random.default_rng(4)
+    kps = (rng.uniform(-1200, 1200, (2, 17, 3)) + np.array([0, 0, 900.0])).astype(np.float32)
+    idx = mloss.nearest_voxel(vb.coords.to(device), _t(kps, device))
+    np.testing.assert_array_equal(idx.cpu().numpy(), restate_np.nearest_voxel(vb.coords.numpy(), kps))

@@ -163,3 +163,23 @@ def test_coord_volume_numpy_recipe(golden):
     for case, kind, cmu in (("coco_eval", "coco", False), ("coco_train", "coco", False), ("mpii_cmu", "mpii", True)):
         cv = restate_np.coord_volumes(d["base"], 2500.0, 16, d[f"theta_{case}"], kind, cmu)
         np.testing.assert_array_equal(cv, d[f"cv_{case}"])
+
+
+def test_ce_loss_oracles(golden):
+    """VolumetricCELoss (loss.py:52-80): the torch restatement reproduces the reference's
+    loss and gradient; the squared-distance argmin (the kernel's rule) selects exactly the
+    voxels where the reference's gradient is non-zero."""
+    d = golden("ce_loss.npz")
+    vol = torch.from_numpy(d["vol"]).requires_grad_(True)
+    loss = restate_torch.volumetric_ce_loss(torch.from_numpy(d["coords"]), vol, torch.from_numpy(d["kps"]),
+                                            torch.from_numpy(d["validity"]))
+    loss.backward()
+    np.testing.assert_array_equal(loss.detach().numpy(), d["loss"])
+    np.testing.assert_array_equal(vol.grad.numpy(), d["grad_vol"])
+    idx = restate_np.nearest_voxel(d["coords"], d["kps"])
+    g = d["grad_vol"].reshape(2, 17, -1)
+    valid = d["validity"][..., 0] > 0
+    for b in range(2):
+        for j in range(17):
+            if valid[b, j]:
+                assert np.flatnonzero(g[b, j]).tolist() == [idx[b, j]]

@@ -17,6 +17,8 @@
  *                           volume loop feeding unproject and soft-argmax)
  *   mvn_nearest_voxel    <- mvn/models/loss.py:63-67 (VolumetricCELoss's distance volume +
  *                           argmin)
+ *   mvn_v2v_front        <- mvn/models/v2v.py:7-17, 145-146 (V2VModel.front_layers[0] =
+ *                           Basic3DBlock(32, 16, 7), eval mode; BASELINE config 5)
  *
  * Conventions
  *   - Every buffer is caller-owned device memory (hipMalloc / torch), contiguous,
@@ -50,6 +52,10 @@ extern "C" {
 /* ---- dtypes ------------------------------------------------------------ */
 #define MVN_DTYPE_F32   0
 #define MVN_DTYPE_BF16  1
+
+/* ---- volume layouts ------------------------------------------------------ */
+#define MVN_LAYOUT_NCDHW 0     /* (B, C, Vx, Vy, Vz): the reference's unproject output */
+#define MVN_LAYOUT_NDHWC 1     /* (B, Vx, Vy, Vz, C): channels-last (V2V front input)  */
 
 /* ---- view aggregation (op.py:147-161) ---------------------------------- */
 #define MVN_AGG_SUM      0     /* 'sum'                                           */
@@ -121,6 +127,30 @@ int mvn_softargmax3d(const void* vol, int vol_dtype,
  */
 int mvn_dlt(const float* proj, const float* pts, const float* conf, float* out,
             int B, int N, int J, void* stream);
+
+/*
+ * mvn_unproject with a selectable output layout: out_layout = MVN_LAYOUT_NCDHW is exactly
+ * mvn_unproject; MVN_LAYOUT_NDHWC writes (B, Vx, Vy, Vz, C) (C % 4 == 0, N <= 8), the
+ * input layout of mvn_v2v_front.
+ */
+int mvn_unproject_ex(const void* feat, int feat_dtype,
+                     const float* proj, const float* coords, const float* conf,
+                     void* out, int out_dtype, int out_layout,
+                     int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+                     int agg, int align_corners, void* stream);
+
+/*
+ * V2V front block, eval mode: Conv3d(32 -> 16, k = 7, pad = 3) + BatchNorm3d + ReLU
+ * (v2v.py:7-17) on bf16 MFMA, f32 accumulation.
+ *   vol_cl         (B, V, V, V, 32) bf16 channels-last (mvn_unproject_ex NDHWC output)
+ *   weight_packed  mvn_v2v_front_packed_weight_bytes() bytes: bf16 weights as
+ *                  [tap = (dx*7 + dy)*7 + dz][lane 0..63][j 0..7] = W[lane & 15][8*(lane >> 4) + j][dx][dy][dz]
+ *   scale, shift   (16) f32: BN folded, y = relu(conv * scale + shift)
+ *   out            (B, 16, V, V, V) out_dtype (f32 | bf16);  V % 16 == 0
+ */
+size_t mvn_v2v_front_packed_weight_bytes(void);
+int mvn_v2v_front(const void* vol_cl, const void* weight_packed, const float* scale, const float* shift,
+                  void* out, int out_dtype, int B, int V, void* stream);
 
 /*
  * 2D soft-argmax of heatmaps.  Replaces mvn/utils/op.py:11-47 (integrate_tensor_2d) with

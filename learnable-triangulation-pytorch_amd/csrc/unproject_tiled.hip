@@ -196,7 +196,7 @@ __global__ __launch_bounds__(TileShape<NV>::THREADS)
 __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ conf, TOut* __restrict__ out, int B, int n_views, int C, int H, int W, int Vx,
-    int Vy, int Vz, int align_corners, int budget) {
+    int Vy, int Vz, int align_corners, int budget, int out_cl) {
   const int N = EXACT ? NV : n_views;
   using S = TileShape<NV>;
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ, kThreads = S::THREADS, kBuf = S::SLOTS;
@@ -337,7 +337,8 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
   if (npass < 0) {
     // A single footprint exceeds the LDS buffer: gather straight from global memory.
     if (act)
-      gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + vox, nvox, N, C, H, W, cx, cy, cz,
+      gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + (out_cl ? size_t(vox) * C : vox),
+                                   out_cl ? 1 : nvox, N, C, H, W, cx, cy, cz,
                                    align_corners);
     return;
   }
@@ -374,7 +375,29 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
       if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight
     }
   };
+  // out_cl (channels-last (B, Vx, Vy, Vz, C) output, C % 4 == 0; the V2V front block's input
+  // layout): one 16-byte (f32) / 8-byte (bf16) store of the group's 4 channels per voxel.
+  const uint32_t ooff_cl = act ? uint32_t(vox) * uint32_t(C) * uint32_t(sizeof(TOut)) : kOob;
   auto aggregate_store = [&](int c0, const float (&sv)[G][NV]) {
+    if (out_cl) {
+      float r[G];
+#pragma unroll
+      for (int ch = 0; ch < G; ++ch) r[ch] = aggregate_fast<AGG, NV>(sv[ch], N, cfb ? cfb + c0 + ch : nullptr, C);
+      const uint32_t soff = uint32_t(c0) * uint32_t(sizeof(TOut));
+      if constexpr (sizeof(TOut) == 4) {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
+                               make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]),
+                                          __float_as_uint(r[3]))),
+            ors, ooff_cl, soff, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int,
+                               make_uint2(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[2], r[3]))),
+            ors, ooff_cl, soff, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int ch = 0; ch < G; ++ch) {
       const int c = c0 + ch;
@@ -476,7 +499,8 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
 
 template <int AGG, typename TIn, typename TOut>
 int launch_tiled(const void* feat, const float* P, const float* coords, const float* conf, void* out, int B,
-                 int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, hipStream_t s) {
+                 int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, int out_cl, hipStream_t s) {
+  if (out_cl && C % 4 != 0) return MVN_ERR_SHAPE;
   // 32-bit buffer offsets: a frame's maps and volume must stay below 2 GiB
   if ((long long)N * C * H * W * sizeof(TIn) >= (1LL << 31) ||
       (long long)C * Vx * Vy * Vz * sizeof(TOut) >= (1LL << 31))
@@ -493,7 +517,7 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
     if (nb > INT_MAX) return false;
     unproject_tiled<AGG, TIn, TOut, NV, decltype(exact)::value><<<int(nb), S::THREADS, 0, s>>>(
         static_cast<const TIn*>(feat), P, coords, conf, static_cast<TOut*>(out), B, N, C, H, W, Vx, Vy, Vz,
-        align_corners, budget);
+        align_corners, budget, out_cl);
     return true;
   };
   using I4 = std::integral_constant<int, 4>;
@@ -507,12 +531,12 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
 
 #define MVN_INSTANTIATE(AGG)                                                                                   \
   template int launch_tiled<AGG, float, float>(const void*, const float*, const float*, const float*, void*,    \
-                                               int, int, int, int, int, int, int, int, int, hipStream_t);       \
+                                               int, int, int, int, int, int, int, int, int, int, hipStream_t);       \
   template int launch_tiled<AGG, uint16_t, uint16_t>(const void*, const float*, const float*, const float*,     \
-                                                     void*, int, int, int, int, int, int, int, int, int,        \
+                                                     void*, int, int, int, int, int, int, int, int, int, int,   \
                                                      hipStream_t);                                              \
   template int launch_tiled<AGG, uint16_t, float>(const void*, const float*, const float*, const float*, void*, \
-                                                  int, int, int, int, int, int, int, int, int, hipStream_t);
+                                                  int, int, int, int, int, int, int, int, int, int, hipStream_t);
 MVN_INSTANTIATE(MVN_AGG_SUM)
 MVN_INSTANTIATE(MVN_AGG_MAX)
 MVN_INSTANTIATE(MVN_AGG_SOFTMAX)

@@ -1,0 +1,139 @@
+// V2V front block on bf16 MFMA for gfx950 (BASELINE config 5).
+//
+// Replaces V2VModel.front_layers[0] = Basic3DBlock(32, 16, 7) of mvn/models/v2v.py:7-17
+// (Conv3d 32 -> 16, kernel 7, stride 1, padding 3, then BatchNorm3d and ReLU) in eval
+// mode: BN folded by the host into a per-channel scale and shift (conv bias included).
+// Input: the unprojected volume channels-last (B, V, V, V, 32) bf16 — the unprojection
+// writes that layout directly (mvn_unproject_ex, MVN_LAYOUT_NDHWC), so the two launches
+// form the fused unproject + view-softmax + front-block pipeline of config 5.
+//
+// Implicit GEMM, one MFMA per (16 output voxels, tap): A = 16 z-consecutive voxels x 32
+// input channels (the tap-shifted input, read from an LDS halo), B = the tap's 32 x 16
+// weights (prepacked [tap][cout][cin], straight from L2 into registers, one tap ahead),
+// C = 16 voxels x 16 output channels in f32.  A block owns a 4 x 4 x 16 output tile: its
+// 10 x 10 x 22-voxel input halo (140,800 B of LDS, zero-padded at the volume border like
+// Conv3d's padding=3) is staged once; each of the 4 waves takes one x-row of the tile
+// (4 M-blocks = 4 accumulators) and walks the 343 taps.  Per tap and wave: 1 global 16-B
+// weight load and 4 x (ds_read_b128 + v_mfma_f32_16x16x32_bf16).
+// Arithmetic: 2 * 32 * 16 * 343 * V^3 flop per frame (92.1 GFLOP at V = 64): MFMA-bound.
+#include <climits>
+
+#include "common.hpp"
+
+namespace mvn {
+namespace {
+
+constexpr int CI = 32, CO = 16, KS = 7, PAD = 3, NTAP = KS * KS * KS;
+constexpr int TX = 4, TY = 4, TZ = 16;
+constexpr int HX = TX + KS - 1, HY = TY + KS - 1, HZ = TZ + KS - 1;   // 10, 10, 22
+constexpr int HVOX = HX * HY * HZ;                                     // 2200 voxels, 64 B each
+constexpr int kThreads = 256;
+constexpr uint32_t kOob = 0x80000000u;
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(a >> 32));
+  void* p = reinterpret_cast<void*>((uint64_t(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, int(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
+}
+
+template <typename TO>
+__global__ __launch_bounds__(kThreads) void v2v_front(const uint16_t* __restrict__ in, const uint4* __restrict__ wpk,
+                                                     const float* __restrict__ scale, const float* __restrict__ shift,
+                                                     TO* __restrict__ out, int V) {
+  __shared__ uint4 halo[HVOX * 4];          // [hx][hy][hz][8-channel chunk]
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const int nTz = V / TZ, nTy = V / TY, nTx = V / TX;
+  int L = blockIdx.x;
+  const int tz = L % nTz; L /= nTz;
+  const int ty = L % nTy; L /= nTy;
+  const int tx = L % nTx;
+  const int b = L / nTx;
+  const int x0 = tx * TX, y0 = ty * TY, z0 = tz * TZ;
+  const size_t nvox = size_t(V) * V * V;
+
+  // ---- stage the input halo (zero outside the volume) ----------------------------
+  const __amdgpu_buffer_rsrc_t irs = make_rsrc(in + size_t(b) * nvox * CI, uint32_t(nvox * CI * 2));
+  for (int q = t; q < HVOX * 4; q += kThreads) {
+    const int v = q >> 2, c = q & 3;
+    const int hz = v % HZ, hy = (v / HZ) % HY, hx = v / (HZ * HY);
+    const int gx = x0 + hx - PAD, gy = y0 + hy - PAD, gz = z0 + hz - PAD;
+    const bool ok = (unsigned(gx) < unsigned(V)) & (unsigned(gy) < unsigned(V)) & (unsigned(gz) < unsigned(V));
+    const uint32_t off = ok ? uint32_t(((size_t(gx) * V + gy) * V + gz) * CI * 2 + c * 16) : kOob;
+    halo[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(irs, off, 0, 0));
+  }
+  __syncthreads();
+
+  // ---- 343 taps x 4 M-blocks per wave ---------------------------------------------
+  const int r = lane & 15, kb = lane >> 4;
+  f32x4_t acc[TY];
+#pragma unroll
+  for (int m = 0; m < TY; ++m) acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const uint4* wl = wpk + lane;              // [tap][64 lanes]: lane's 16 B of the tap's B fragment
+  uint4 bnext = wl[0];
+  for (int dx = 0; dx < KS; ++dx) {
+    for (int dy = 0; dy < KS; ++dy) {
+      // halo byte offset of (w + dx, dy, r) + this lane's channel chunk; m and dz are immediates
+      const uint32_t base = uint32_t((((w + dx) * HY + dy) * HZ + r) * 4 + kb) * 16u;
+      const char* hb = reinterpret_cast<const char*>(halo) + base;
+#pragma unroll
+      for (int dz = 0; dz < KS; ++dz) {
+        const int tap = (dx * KS + dy) * KS + dz;
+        const uint4 bcur = bnext;
+        if (tap + 1 < NTAP) bnext = wl[(tap + 1) * kWave];
+        const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, bcur);
+#pragma unroll
+        for (int m = 0; m < TY; ++m) {
+          const uint4 a = *reinterpret_cast<const uint4*>(hb + (m * HZ + dz) * 64);
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), bf, acc[m], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: folded BN + ReLU, 4 consecutive z of one output channel per lane ----
+  const int co = lane & 15, zr = (lane >> 4) * 4;
+  const float s = scale[co], sh = shift[co];
+#pragma unroll
+  for (int m = 0; m < TY; ++m) {
+    float y[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = fmaxf(__builtin_fmaf(acc[m][i], s, sh), 0.f);
+    TO* o = out + (((size_t(b) * CO + co) * V + (x0 + w)) * V + (y0 + m)) * V + z0 + zr;
+    if constexpr (sizeof(TO) == 4) {
+      *reinterpret_cast<float4*>(o) = make_float4(y[0], y[1], y[2], y[3]);
+    } else {
+      *reinterpret_cast<uint2*>(o) = make_uint2(pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3]));
+    }
+  }
+}
+
+}  // namespace
+}  // namespace mvn
+
+extern "C" size_t mvn_v2v_front_packed_weight_bytes(void) { return size_t(mvn::NTAP) * 64 * 16; }
+
+extern "C" int mvn_v2v_front(const void* vol_cl, const void* weight_packed, const float* scale, const float* shift,
+                             void* out, int out_dtype, int B, int V, void* stream) {
+  using namespace mvn;
+  if (!vol_cl || !weight_packed || !scale || !shift || !out) return MVN_ERR_ARG;
+  if (B <= 0 || V <= 0 || V % TZ != 0 || V % TX != 0 || V % TY != 0) return MVN_ERR_SHAPE;
+  if ((long long)V * V * V * CI * 2 >= (1LL << 31)) return MVN_ERR_SHAPE;
+  const long long nblk = (long long)B * (V / TX) * (V / TY) * (V / TZ);
+  if (nblk > INT_MAX) return MVN_ERR_SHAPE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const auto* in = static_cast<const uint16_t*>(vol_cl);
+  const auto* w = static_cast<const uint4*>(weight_packed);
+  if (out_dtype == MVN_DTYPE_F32)
+    v2v_front<float><<<int(nblk), kThreads, 0, s>>>(in, w, scale, shift, static_cast<float*>(out), V);
+  else if (out_dtype == MVN_DTYPE_BF16)
+    v2v_front<uint16_t><<<int(nblk), kThreads, 0, s>>>(in, w, scale, shift, static_cast<uint16_t*>(out), V);
+  else
+    return MVN_ERR_DTYPE;
+  return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
+}

@@ -1,0 +1,99 @@
+"""V2V front block on the GPU (BASELINE config 5).
+
+``V2VModel.front_layers[0]`` is ``Basic3DBlock(32, 16, 7)`` (mvn/models/v2v.py:7-17,
+145-146): Conv3d 32 -> 16, kernel 7, padding 3, BatchNorm3d, ReLU, applied to the
+unprojected volume (triangulation.py:352).  In eval mode the block is one MFMA kernel
+(csrc/v2v_front.hip) with the BatchNorm folded into a per-channel scale / shift, reading
+the volume channels-last in bf16 straight from the unprojection
+(``unproject_channels_last``): the unproject + view-softmax + front-block pipeline of
+config 5 is two launches and one (B, V^3, 32) bf16 intermediate.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import _lib
+from ._ops import _require_gpu, _stream
+from .op import aggregation_code
+
+CIN, COUT, KS = 32, 16, 7
+
+
+def fold_basic3d_block(weight, bias, bn_weight, bn_bias, running_mean, running_var, eps=1e-5, device="cuda"):
+    """Eval-mode Basic3DBlock parameters -> (packed bf16 weights, scale, shift) on ``device``.
+
+    y = relu(bn(conv(x) + bias)) = relu(conv(x) * s + ((bias - mean) * s + beta)),
+    s = gamma / sqrt(var + eps), folded in float64.  The weights are rounded to bf16 (the
+    kernel's MFMA operand type) and packed [tap][lane][8] as mvn_v2v_front expects."""
+    w = weight.detach().to(torch.float64).cpu()
+    if tuple(w.shape) != (COUT, CIN, KS, KS, KS):
+        raise RuntimeError(f"expected a ({COUT}, {CIN}, 7, 7, 7) Conv3d weight, got {tuple(w.shape)}")
+    s = bn_weight.detach().double().cpu() / torch.sqrt(running_var.detach().double().cpu() + eps)
+    b = bias.detach().double().cpu() if bias is not None else torch.zeros(COUT, dtype=torch.float64)
+    shift = (b - running_mean.detach().double().cpu()) * s + bn_bias.detach().double().cpu()
+    wt = w.reshape(COUT, CIN, KS ** 3).permute(2, 0, 1)                 # [tap][cout][cin]
+    lane = torch.arange(64)
+    cout, kblk = lane % 16, lane // 16
+    cin = kblk.view(64, 1) * 8 + torch.arange(8).view(1, 8)            # [lane][j]
+    packed = wt[:, cout.view(64, 1).expand(64, 8), cin]                 # [tap][lane][j]
+    packed = packed.to(torch.float32).to(torch.bfloat16).contiguous()
+    dev = torch.device(device)
+    return packed.to(dev), s.float().to(dev), shift.float().to(dev)
+
+
+def v2v_front(vol_cl, packed, scale, shift, out_dtype=torch.float32):
+    """(B, V, V, V, 32) bf16 channels-last -> (B, 16, V, V, V) relu(bn(conv3d_7(x)))."""
+    if vol_cl.dtype != torch.bfloat16 or vol_cl.dim() != 5 or vol_cl.shape[-1] != CIN:
+        raise RuntimeError(f"vol_cl must be (B, V, V, V, {CIN}) bfloat16, got {tuple(vol_cl.shape)} {vol_cl.dtype}")
+    B, V = vol_cl.shape[0], vol_cl.shape[1]
+    if tuple(vol_cl.shape[1:4]) != (V, V, V):
+        raise RuntimeError("v2v_front needs a cubic volume")
+    x = vol_cl.contiguous()
+    _require_gpu(x, packed, scale, shift)
+    out = torch.empty((B, COUT, V, V, V), dtype=out_dtype, device=x.device)
+    code = _lib.load().mvn_v2v_front(x.data_ptr(), packed.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                                     out.data_ptr(), 0 if out_dtype == torch.float32 else 1, B, V, _stream(x))
+    _lib.check(code, "mvn_v2v_front")
+    return out
+
+
+def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggregation_method="softmax",
+                            out_dtype=torch.bfloat16, align_corners=False):
+    """unproject_heatmaps (op.py:99-163) written channels-last: (B, Vx, Vy, Vz, C)."""
+    agg = aggregation_code(volume_aggregation_method)
+    if agg == _lib.MVN_AGG_CONF:
+        raise ValueError("unproject_channels_last: 'conf*' aggregation is not supported here")
+    feat = heatmaps.contiguous()
+    proj = proj_matricies.float().contiguous()
+    coords = coord_volumes.float().contiguous()
+    _require_gpu(feat, proj, coords)
+    B, N, C, H, W = feat.shape
+    Vx, Vy, Vz = coords.shape[1:4]
+    out = torch.empty((B, Vx, Vy, Vz, C), dtype=out_dtype, device=feat.device)
+    fd = 0 if feat.dtype == torch.float32 else 1
+    od = 0 if out_dtype == torch.float32 else 1
+    code = _lib.load().mvn_unproject_ex(feat.data_ptr(), fd, proj.data_ptr(), coords.data_ptr(), None,
+                                        out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC, B, N, C, H, W, Vx, Vy, Vz, agg,
+                                        int(align_corners), _stream(feat))
+    _lib.check(code, "mvn_unproject_ex")
+    return out
+
+
+class Basic3DBlockFront(nn.Module):
+    """Eval-mode replacement of Basic3DBlock(32, 16, 7) on a channels-last bf16 volume."""
+
+    def __init__(self, packed, scale, shift):
+        super().__init__()
+        self.register_buffer("packed", packed)
+        self.register_buffer("scale", scale)
+        self.register_buffer("shift", shift)
+
+    @classmethod
+    def from_reference(cls, block, device="cuda"):
+        conv, bn = block.block[0], block.block[1]
+        return cls(*fold_basic3d_block(conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean,
+                                       bn.running_var, bn.eps, device=device))
+
+    def forward(self, vol_cl, out_dtype=torch.float32):
+        return v2v_front(vol_cl, self.packed, self.scale, self.shift, out_dtype)

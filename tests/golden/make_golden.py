@@ -2,7 +2,7 @@
 
 Run in the build container only (it needs /root/reference; the GPU box never runs it):
 
-    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes|ce_loss]   (argument: only that fixture)
+    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes|ce_loss|v2v_front]   (argument: only that fixture)
 
 The reference (learnable-triangulation-pytorch, mvn/utils/op.py and
 mvn/utils/multiview.py) is imported read-only with two in-memory accommodations:
@@ -178,8 +178,33 @@ def golden_ce_loss():
          loss=loss.detach().numpy(), grad_vol=vol.grad.numpy())
 
 
+def golden_v2v_front():
+    """V2VModel.front_layers[0] = Basic3DBlock(32, 16, 7) (v2v.py:7-17) in eval mode with
+    seeded parameters; conv weights and the input volume rounded to bf16 (the MFMA operand
+    type), so the kernel and the reference differ only in f32 accumulation order."""
+    from mvn.models.v2v import Basic3DBlock  # noqa: WPS433 (reference)
+    g = torch.Generator().manual_seed(41)
+    blk = Basic3DBlock(32, 16, 7).eval()
+    with torch.no_grad():
+        conv, bn = blk.block[0], blk.block[1]
+        conv.weight.copy_((torch.randn(conv.weight.shape, generator=g) * 0.02).bfloat16().float())
+        conv.bias.copy_(torch.randn(16, generator=g) * 0.1)
+        bn.weight.copy_(torch.rand(16, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(16, generator=g) * 0.1)
+        bn.running_mean.copy_(torch.randn(16, generator=g) * 0.1)
+        bn.running_var.copy_(torch.rand(16, generator=g) + 0.5)
+        x = torch.randn((2, 32, 16, 16, 16), generator=g).bfloat16().float()
+        y = blk(x)
+    save("v2v_front.npz", x=x.numpy(), weight=conv.weight.detach().numpy(), bias=conv.bias.detach().numpy(),
+         bn_weight=bn.weight.detach().numpy(), bn_bias=bn.bias.detach().numpy(), bn_mean=bn.running_mean.numpy(),
+         bn_var=bn.running_var.numpy(), eps=np.float64(bn.eps), y=y.numpy())
+
+
 def main():
     op, multiview = import_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "v2v_front":
+        golden_v2v_front()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "ce_loss":
         golden_ce_loss()
         return
@@ -284,6 +309,7 @@ def main():
     golden_softargmax2d(op)
     golden_coord_volumes()
     golden_ce_loss()
+    golden_v2v_front()
 
 
 if __name__ == "__main__":

@@ -26,7 +26,7 @@ def lib():
 def test_header_declares_the_three_entry_points():
     fns = header_functions()
     for name in ("mvn_unproject", "mvn_softargmax3d", "mvn_dlt", "mvn_softargmax2d", "mvn_coord_volumes",
-                 "mvn_nearest_voxel",
+                 "mvn_nearest_voxel", "mvn_unproject_ex", "mvn_v2v_front",
                  "mvn_softargmax3d_workspace_bytes",
                  "mvn_strerror", "mvn_version"):
         assert name in fns

@@ -366,3 +366,44 @@ def test_nearest_voxel_full_size(device):
     kps = (rng.uniform(-1200, 1200, (2, 17, 3)) + np.array([0, 0, 900.0])).astype(np.float32)
     idx = mloss.nearest_voxel(vb.coords.to(device), _t(kps, device))
     np.testing.assert_array_equal(idx.cpu().numpy(), restate_np.nearest_voxel(vb.coords.numpy(), kps))
+
+
+# ----------------------------------------------------------------------------- V2V front block (config 5)
+def test_v2v_front_matches_reference_golden(golden, device):
+    from mvn_rocm import v2v
+    d = golden("v2v_front.npz")
+    t = {k: torch.from_numpy(np.asarray(d[k])) for k in ("weight", "bias", "bn_weight", "bn_bias", "bn_mean", "bn_var")}
+    blk = v2v.Basic3DBlockFront(*v2v.fold_basic3d_block(t["weight"], t["bias"], t["bn_weight"], t["bn_bias"],
+                                                         t["bn_mean"], t["bn_var"], float(d["eps"]), device=device))
+    x_cl = _t(d["x"], device).permute(0, 2, 3, 4, 1).contiguous().to(torch.bfloat16)
+    y = blk(x_cl)
+    assert y.shape == (2, 16, 16, 16, 16)
+    assert max_rel(y.cpu().numpy(), d["y"]) <= 1e-4          # bf16 operands, f32 accumulation order only
+    y16 = blk(x_cl, out_dtype=torch.bfloat16)
+    np.testing.assert_allclose(y16.float().cpu().numpy(), d["y"], rtol=2 ** -7, atol=2 ** -7 * np.abs(d["y"]).max())
+
+
+def test_unproject_channels_last_is_a_transpose(device):
+    from mvn_rocm import synth, v2v
+    vb = synth.volumetric_batch(2, channels=32, volume=32, dtype=torch.bfloat16, device=device, seed=12)
+    ref = _op().unproject_heatmaps(vb.features, vb.proj, vb.coords, "softmax")
+    cl = v2v.unproject_channels_last(vb.features, vb.proj, vb.coords, "softmax")
+    torch.testing.assert_close(cl, ref.permute(0, 2, 3, 4, 1), rtol=0, atol=0)
+    ref32 = _op().unproject_heatmaps(vb.features, vb.proj, vb.coords, "sum", out_dtype=torch.float32)
+    cl32 = v2v.unproject_channels_last(vb.features, vb.proj, vb.coords, "sum", out_dtype=torch.float32)
+    torch.testing.assert_close(cl32, ref32.permute(0, 2, 3, 4, 1), rtol=0, atol=0)
+
+
+def test_v2v_front_full_size_vs_torch_cpu(device):
+    import torch.nn.functional as F
+    from mvn_rocm import v2v
+    g = torch.Generator().manual_seed(5)
+    w = (torch.randn((16, 32, 7, 7, 7), generator=g) * 0.02).bfloat16().float()
+    b, gam, bet = torch.randn(16, generator=g) * 0.1, torch.rand(16, generator=g) + 0.5, torch.randn(16, generator=g)
+    mean, var = torch.randn(16, generator=g) * 0.1, torch.rand(16, generator=g) + 0.5
+    x = torch.randn((1, 32, 32, 32, 32), generator=g).bfloat16().float()
+    packed, scale, shift = v2v.fold_basic3d_block(w, b, gam, bet, mean, var, 1e-5, device=device)
+    y = v2v.v2v_front(x.permute(0, 2, 3, 4, 1).contiguous().to(device).to(torch.bfloat16), packed, scale, shift)
+    ref = torch.relu(F.conv3d(x, w, None, padding=3) * scale.cpu().view(1, -1, 1, 1, 1)
+                     + shift.cpu().view(1, -1, 1, 1, 1))
+    assert max_rel(y.cpu().numpy(), ref.numpy()) <= 1e-4

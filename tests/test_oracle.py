@@ -183,3 +183,21 @@ def test_ce_loss_oracles(golden):
         for j in range(17):
             if valid[b, j]:
                 assert np.flatnonzero(g[b, j]).tolist() == [idx[b, j]]
+
+
+def test_v2v_front_folding_and_packing(golden):
+    """Eval-mode Basic3DBlock(32, 16, 7) = relu(conv * s + shift) with the BN folded in
+    float64 (mvn_rocm.v2v.fold_basic3d_block); the packed MFMA B operands hold
+    W[lane & 15][8 * (lane >> 4) + j][tap]."""
+    import torch.nn.functional as F
+    from mvn_rocm import v2v
+    d = golden("v2v_front.npz")
+    t = {k: torch.from_numpy(np.asarray(d[k])) for k in ("weight", "bias", "bn_weight", "bn_bias", "bn_mean", "bn_var")}
+    packed, scale, shift = v2v.fold_basic3d_block(t["weight"], t["bias"], t["bn_weight"], t["bn_bias"], t["bn_mean"],
+                                                  t["bn_var"], float(d["eps"]), device="cpu")
+    conv = F.conv3d(torch.from_numpy(d["x"]), t["weight"], None, padding=3)
+    y = torch.relu(conv * scale.view(1, -1, 1, 1, 1) + shift.view(1, -1, 1, 1, 1))
+    assert max_rel(y.numpy(), d["y"]) <= 1e-5
+    w = t["weight"].reshape(16, 32, 343)
+    for tap, lane, j in ((0, 0, 0), (123, 37, 5), (342, 63, 7), (200, 16, 0)):
+        assert float(packed[tap, lane, j]) == float(w[lane % 16, 8 * (lane // 16) + j, tap].bfloat16())

@@ -8,6 +8,10 @@ over channels [0:17] of the unprojected volume (the stand-in for V2V, SURVEY.md 
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--no-cpu-baseline]
 
+With the default --config 2 the line also carries `secondary` (config 3, bf16, 32 frames)
+and `config5` (unproject written channels-last + the V2V front Conv3d block on bf16 MFMA,
+64 frames, with its own MFMA roofline); --no-secondary drops both.
+
 N > 1 is launched by torch.distributed.run (one process per GPU); every rank builds its
 own frames from (seed, global frame index) — weak scaling, fixed frames per GPU.
 Rank 0 prints ONE JSON line.
@@ -40,7 +44,12 @@ CONFIGS = {
               label="cfg3: 4 views x 32 ch x 96^2 -> 64^3 unproject(softmax agg) + 17-joint soft-argmax, bf16"),
     "4": dict(views=8, channels=32, heatmap=96, volume=64, joints=17, frames=16, dtype=torch.float32,
               label="cfg4: 8 views (CMU-style) x 32 ch x 96^2 -> 64^3 unproject + soft-argmax, fp32"),
+    "5": dict(views=4, channels=32, heatmap=96, volume=64, joints=17, frames=64, dtype=torch.bfloat16,
+              label="cfg5: 4 views x 32 ch x 96^2 -> 64^3 unproject(softmax agg, channels-last bf16) + V2V front "
+                    "Basic3DBlock(32,16,7) conv3d+BN+ReLU on bf16 MFMA"),
 }
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 (no sparsity)
+V2V_FLOP_PER_FRAME = 2 * 32 * 16 * 343 * 64 ** 3
 
 
 def unproject_bytes(c, E):
@@ -143,6 +152,60 @@ def run_config(name, args, rank, world, device):
         path_gbps=frame_bytes(cfg, E) * frames_total / elapsed / 1e9)
 
 
+def run_config5(args, rank, world, device):
+    """Config 5: unproject (softmax, written channels-last bf16) + V2V front block on MFMA;
+    roofline of the front block against the bf16 dense MFMA peak."""
+    from mvn_rocm import v2v
+    cfg = CONFIGS["5"]
+    B = cfg["frames"]
+    vb = synth.volumetric_batch(B, n_views=cfg["views"], channels=cfg["channels"], heatmap=cfg["heatmap"],
+                                volume=cfg["volume"], dtype=cfg["dtype"], device=device, seed=0, first_frame=rank * B)
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn((16, 32, 7, 7, 7), generator=g) * 0.02
+    packed, scale, shift = v2v.fold_basic3d_block(w, torch.randn(16, generator=g) * 0.1, torch.rand(16, generator=g) + 0.5,
+                                                  torch.randn(16, generator=g) * 0.1, torch.zeros(16), torch.ones(16),
+                                                  device=device)
+    ev = []
+
+    def step(timed=False):
+        cl = v2v.unproject_channels_last(vb.features, vb.proj, vb.coords, "softmax")
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        y = v2v.v2v_front(cl, packed, scale, shift, torch.bfloat16)
+        if timed:
+            e1.record()
+            ev.append((e0, e1))
+        return y
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    conv_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    tflops = V2V_FLOP_PER_FRAME * B / (conv_ms * 1e-3) / 1e12
+    return dict(workload=cfg["label"], value=B * world * args.steps / elapsed, unit="frames/s",
+                ms_per_step=elapsed / args.steps * 1e3, frames_per_gpu=B, dtype="bf16",
+                roofline={"kernel": "v2v_front<bf16> (Conv3d 32->16 k7 + BN + ReLU)", "bound": "mfma",
+                          "achieved": tflops, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": tflops / MFMA_BF16_PEAK_TFLOPS, "launch_ms": conv_ms,
+                          "flop_per_launch": V2V_FLOP_PER_FRAME * B})
+
+
 def cpu_baseline(seconds=15.0):
     """The reference algorithm restated op-for-op in torch-CPU (oracle/restate_torch.py),
     timed on this host on one frame of config 2 at a time (bounded sample)."""
@@ -169,7 +232,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="2", choices=[k for k in sorted(CONFIGS) if k != "5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     args = ap.parse_args()
@@ -191,6 +254,9 @@ def main():
                          unproject_achieved_gbps=s["achieved_gbps"],
                          unproject_frac=s["achieved_gbps"] / HBM_PEAK_GBPS,
                          path_algorithmic_gbps=s["path_gbps"], path_frac=s["path_gbps"] / HBM_PEAK_GBPS)
+    cfg5 = None
+    if not args.no_secondary and args.config == "2":
+        cfg5 = run_config5(args, rank, world, device)
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base = cpu_baseline()
@@ -223,6 +289,7 @@ def main():
             "path_algorithmic_gbps": r["path_gbps"],
             "cpu_baseline": base,
             "secondary": secondary,
+            "config5": cfg5,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -9,7 +9,7 @@
 //
 // Implicit GEMM, one MFMA per (16 output voxels, tap): A = 16 z-consecutive voxels x 32
 // input channels (the tap-shifted input, read from an LDS halo), B = the tap's 32 x 16
-// weights (prepacked [tap][cout][cin], straight from L2 into registers, one tap ahead),
+// weights (prepacked [tap][cout][cin], straight from L2 into registers, one 7-tap row ahead),
 // C = 16 voxels x 16 output channels in f32.  A block owns a 4 x 4 x 16 output tile: its
 // 10 x 10 x 22-voxel input halo (140,800 B of LDS, zero-padded at the volume border like
 // Conv3d's padding=3) is staged once; each of the 4 waves takes one x-row of the tile
@@ -42,14 +42,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(p, 0, int(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
 }
 
+// LDS swizzle of a halo voxel's four 16-byte channel chunks: chunk c of a voxel at halo z
+// index hz sits at position c ^ swz(hz).  The A-operand read of one MFMA has lanes
+// r = 0..15 (16 z-consecutive voxels) x chunk kb = 0..3; unswizzled, the 64-byte voxel
+// pitch maps voxels 4 apart to the same bank quad (2-way conflicts in every lane group of
+// ds_read_b128); with this swizzle every group hits 16 distinct quads for any z offset
+// (exhaustive check over the four gfx950 lane groups).
+__device__ __forceinline__ int swz(int hz) { return ((hz >> 2) & 1) << 1; }
+
 template <typename TO>
-__global__ __launch_bounds__(kThreads) void v2v_front(const uint16_t* __restrict__ in, const uint4* __restrict__ wpk,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void v2v_front(const uint16_t* __restrict__ in, const uint4* __restrict__ wpk,
                                                      const float* __restrict__ scale, const float* __restrict__ shift,
                                                      TO* __restrict__ out, int V) {
   __shared__ uint4 halo[HVOX * 4];          // [hx][hy][hz][8-channel chunk]
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
   const int nTz = V / TZ, nTy = V / TY, nTx = V / TX;
-  int L = blockIdx.x;
+  // XCD-contiguous block order (cdna_hip_programming.md T1): neighbouring tiles, whose
+  // halos overlap ~8x, run on the same XCD and share its L2.  Every tile costs the same,
+  // so contiguous ranges are balanced.
+  int L = xcd_remap(blockIdx.x, gridDim.x);
   const int tz = L % nTz; L /= nTz;
   const int ty = L % nTy; L /= nTy;
   const int tx = L % nTx;
@@ -59,13 +70,30 @@ __global__ __launch_bounds__(kThreads) void v2v_front(const uint16_t* __restrict
 
   // ---- stage the input halo (zero outside the volume) ----------------------------
   const __amdgpu_buffer_rsrc_t irs = make_rsrc(in + size_t(b) * nvox * CI, uint32_t(nvox * CI * 2));
-  for (int q = t; q < HVOX * 4; q += kThreads) {
-    const int v = q >> 2, c = q & 3;
-    const int hz = v % HZ, hy = (v / HZ) % HY, hx = v / (HZ * HY);
-    const int gx = x0 + hx - PAD, gy = y0 + hy - PAD, gz = z0 + hz - PAD;
-    const bool ok = (unsigned(gx) < unsigned(V)) & (unsigned(gy) < unsigned(V)) & (unsigned(gz) < unsigned(V));
-    const uint32_t off = ok ? uint32_t(((size_t(gx) * V + gy) * V + gz) * CI * 2 + c * 16) : kOob;
-    halo[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(irs, off, 0, 0));
+  // 35 16-byte chunks per thread, issued in batches of 12 so that the loads overlap
+  // (issuing one load per write would expose a full memory latency 35 times).
+  constexpr int kChunks = HVOX * 4, kPer = (kChunks + kThreads - 1) / kThreads, kBatch = 12;
+#pragma unroll
+  for (int i0 = 0; i0 < kPer; i0 += kBatch) {
+    uint4 vals[kBatch];
+    int dst[kBatch];
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      const int q = t + (i0 + u) * kThreads;
+      dst[u] = -1;
+      if (i0 + u < kPer && q < kChunks) {
+        const int v = q >> 2, c = q & 3;
+        const int hz = v % HZ, hy = (v / HZ) % HY, hx = v / (HZ * HY);
+        const int gx = x0 + hx - PAD, gy = y0 + hy - PAD, gz = z0 + hz - PAD;
+        const bool ok = (unsigned(gx) < unsigned(V)) & (unsigned(gy) < unsigned(V)) & (unsigned(gz) < unsigned(V));
+        const uint32_t off = ok ? uint32_t(((size_t(gx) * V + gy) * V + gz) * CI * 2 + c * 16) : kOob;
+        vals[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(irs, off, 0, 0));
+        dst[u] = v * 4 + (c ^ swz(hz));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u)
+      if (dst[u] >= 0) halo[dst[u]] = vals[u];
   }
   __syncthreads();
 
@@ -75,25 +103,43 @@ __global__ __launch_bounds__(kThreads) void v2v_front(const uint16_t* __restrict
 #pragma unroll
   for (int m = 0; m < TY; ++m) acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const uint4* wl = wpk + lane;              // [tap][64 lanes]: lane's 16 B of the tap's B fragment
-  uint4 bnext = wl[0];
-  for (int dx = 0; dx < KS; ++dx) {
-    for (int dy = 0; dy < KS; ++dy) {
-      // halo byte offset of (w + dx, dy, r) + this lane's channel chunk; m and dz are immediates
-      const uint32_t base = uint32_t((((w + dx) * HY + dy) * HZ + r) * 4 + kb) * 16u;
-      const char* hb = reinterpret_cast<const char*>(halo) + base;
+  uint32_t zoff[KS];                         // byte offset of (hz = r + dz, chunk kb) within a halo row
 #pragma unroll
-      for (int dz = 0; dz < KS; ++dz) {
-        const int tap = (dx * KS + dy) * KS + dz;
-        const uint4 bcur = bnext;
-        if (tap + 1 < NTAP) bnext = wl[(tap + 1) * kWave];
-        const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, bcur);
+  for (int dz = 0; dz < KS; ++dz) zoff[dz] = uint32_t(((r + dz) * 4 + (kb ^ swz(r + dz))) * 16);
+  // Software pipeline over the 49 (dx, dy) rows of taps.  With one wave per SIMD (the halo
+  // fills the LDS) nothing else hides latency, so while row i's 28 MFMAs run, row i+1's 28
+  // A fragments (LDS) and 7 B fragments (L2) are already in flight: 2 x 140 VGPRs of
+  // operands, affordable at one wave per SIMD.
+  uint4 acur[KS][TY], anxt[KS][TY], bcur[KS], bnxt[KS];
+  auto load_row = [&](int rowi, uint4 (&a)[KS][TY], uint4 (&bf)[KS]) {
+    const int dx = rowi / KS, dy = rowi - dx * KS;
+    const char* hb = reinterpret_cast<const char*>(halo) + uint32_t(((w + dx) * HY + dy) * HZ * 64);
 #pragma unroll
-        for (int m = 0; m < TY; ++m) {
-          const uint4 a = *reinterpret_cast<const uint4*>(hb + (m * HZ + dz) * 64);
-          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), bf, acc[m], 0, 0, 0);
-        }
-      }
+    for (int dz = 0; dz < KS; ++dz) {
+      bf[dz] = wl[(rowi * KS + dz) * kWave];
+#pragma unroll
+      for (int m = 0; m < TY; ++m) a[dz][m] = *reinterpret_cast<const uint4*>(hb + zoff[dz] + m * HZ * 64);
     }
+  };
+  auto mma_row = [&](const uint4 (&a)[KS][TY], const uint4 (&bf)[KS]) {
+#pragma unroll
+    for (int dz = 0; dz < KS; ++dz)
+#pragma unroll
+      for (int m = 0; m < TY; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[dz][m]),
+                                                         __builtin_bit_cast(bf16x8_t, bf[dz]), acc[m], 0, 0, 0);
+  };
+  load_row(0, acur, bcur);
+  for (int rowi = 0; rowi < KS * KS; rowi += 2) {
+    if (rowi + 1 < KS * KS) load_row(rowi + 1, anxt, bnxt);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_row(acur, bcur);
+    __builtin_amdgcn_sched_barrier(0);
+    if (rowi + 1 >= KS * KS) break;
+    if (rowi + 2 < KS * KS) load_row(rowi + 2, acur, bcur);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_row(anxt, bnxt);
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   // ---- epilogue: folded BN + ReLU, 4 consecutive z of one output channel per lane ----

@@ -10,10 +10,11 @@
 // Implicit GEMM, one MFMA per (16 output voxels, tap): A = 16 z-consecutive voxels x 32
 // input channels (the tap-shifted input, read from an LDS halo), B = the tap's 32 x 16
 // weights (prepacked [tap][cout][cin], straight from L2 into registers, one 7-tap row ahead),
-// C = 16 voxels x 16 output channels in f32.  A block owns a 4 x 4 x 16 output tile: its
-// 10 x 10 x 22-voxel input halo (140,800 B of LDS, zero-padded at the volume border like
-// Conv3d's padding=3) is staged once; each of the 4 waves takes one x-row of the tile
-// (4 M-blocks = 4 accumulators) and walks the 343 taps.  Per tap and wave: 1 global 16-B
+// C = 16 voxels x 16 output channels in f32.  A block walks a column of 4 x 4 x 16 output
+// tiles along x: the 10 x 10 x 22-voxel input halo (140,800 B of LDS, zero-padded at the
+// volume border like Conv3d's padding=3) is a ring of x-slices, 4 new slices per tile; each
+// of the 4 waves takes one x-row of the tile (4 M-blocks = 4 accumulators) and walks the
+// 343 taps.  Per tap and wave: 1 global 16-B
 // weight load and 4 x (ds_read_b128 + v_mfma_f32_16x16x32_bf16).
 // Arithmetic: 2 * 32 * 16 * 343 * V^3 flop per frame (92.1 GFLOP at V = 64): MFMA-bound.
 #include <climits>
@@ -54,107 +55,116 @@ template <typename TO>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void v2v_front(const uint16_t* __restrict__ in, const uint4* __restrict__ wpk,
                                                      const float* __restrict__ scale, const float* __restrict__ shift,
                                                      TO* __restrict__ out, int V) {
-  __shared__ uint4 halo[HVOX * 4];          // [hx][hy][hz][8-channel chunk]
+  __shared__ uint4 halo[HVOX * 4];          // ring of HX x-slices: [slot][hy][hz][8-channel chunk]
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
   const int nTz = V / TZ, nTy = V / TY, nTx = V / TX;
-  // XCD-contiguous block order (cdna_hip_programming.md T1): neighbouring tiles, whose
-  // halos overlap ~8x, run on the same XCD and share its L2.  Every tile costs the same,
-  // so contiguous ranges are balanced.
+  // A block walks one column of tiles along x (nTx tiles): consecutive tiles' halos share
+  // HX - TX = 6 of their 10 x-slices, so per tile only TX = 4 new slices are loaded into a
+  // ring (slot = (gx + PAD) mod HX).  Blocks: (frame, ty, tz), XCD-contiguous.
   int L = xcd_remap(blockIdx.x, gridDim.x);
   const int tz = L % nTz; L /= nTz;
   const int ty = L % nTy; L /= nTy;
-  const int tx = L % nTx;
-  const int b = L / nTx;
-  const int x0 = tx * TX, y0 = ty * TY, z0 = tz * TZ;
+  const int b = L;
+  const int y0 = ty * TY, z0 = tz * TZ;
   const size_t nvox = size_t(V) * V * V;
-
-  // ---- stage the input halo (zero outside the volume) ----------------------------
   const __amdgpu_buffer_rsrc_t irs = make_rsrc(in + size_t(b) * nvox * CI, uint32_t(nvox * CI * 2));
-  // 35 16-byte chunks per thread, issued in batches of 12 so that the loads overlap
-  // (issuing one load per write would expose a full memory latency 35 times).
-  constexpr int kChunks = HVOX * 4, kPer = (kChunks + kThreads - 1) / kThreads, kBatch = 12;
-#pragma unroll
-  for (int i0 = 0; i0 < kPer; i0 += kBatch) {
-    uint4 vals[kBatch];
-    int dst[kBatch];
-#pragma unroll
-    for (int u = 0; u < kBatch; ++u) {
-      const int q = t + (i0 + u) * kThreads;
-      dst[u] = -1;
-      if (i0 + u < kPer && q < kChunks) {
-        const int v = q >> 2, c = q & 3;
-        const int hz = v % HZ, hy = (v / HZ) % HY, hx = v / (HZ * HY);
-        const int gx = x0 + hx - PAD, gy = y0 + hy - PAD, gz = z0 + hz - PAD;
-        const bool ok = (unsigned(gx) < unsigned(V)) & (unsigned(gy) < unsigned(V)) & (unsigned(gz) < unsigned(V));
-        const uint32_t off = ok ? uint32_t(((size_t(gx) * V + gy) * V + gz) * CI * 2 + c * 16) : kOob;
-        vals[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(irs, off, 0, 0));
-        dst[u] = v * 4 + (c ^ swz(hz));
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kBatch; ++u)
-      if (dst[u] >= 0) halo[dst[u]] = vals[u];
-  }
-  __syncthreads();
+  constexpr int kSliceChunks = HY * HZ * 4;                  // 880 chunks of 16 B per x-slice
 
-  // ---- 343 taps x 4 M-blocks per wave ---------------------------------------------
-  const int r = lane & 15, kb = lane >> 4;
-  f32x4_t acc[TY];
+  // load x-slices gx0 .. gx0 + n - 1 (zero outside the volume) into their ring slots;
+  // batches of 14 loads per thread in flight before the LDS writes
+  auto load_slices = [&](int gx0, int n) {
+    const int total = n * kSliceChunks;
+    constexpr int kBatch = 14;
+    for (int i0 = 0; i0 * kThreads < total; i0 += kBatch) {
+      uint4 vals[kBatch];
+      int dst[kBatch];
 #pragma unroll
-  for (int m = 0; m < TY; ++m) acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < kBatch; ++u) {
+        const int q = t + (i0 + u) * kThreads;
+        dst[u] = -1;
+        if (q < total) {
+          const int sl = q / kSliceChunks, rem = q - sl * kSliceChunks;
+          const int v = rem >> 2, c = rem & 3;
+          const int hz = v % HZ, hy = v / HZ;
+          const int gx = gx0 + sl, gy = y0 + hy - PAD, gz = z0 + hz - PAD;
+          const bool ok = (unsigned(gx) < unsigned(V)) & (unsigned(gy) < unsigned(V)) & (unsigned(gz) < unsigned(V));
+          const uint32_t off = ok ? uint32_t(((size_t(gx) * V + gy) * V + gz) * CI * 2 + c * 16) : kOob;
+          vals[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(irs, off, 0, 0));
+          const int slot = (gx + PAD) % HX;
+          dst[u] = slot * kSliceChunks + v * 4 + (c ^ swz(hz));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u)
+        if (dst[u] >= 0) halo[dst[u]] = vals[u];
+    }
+  };
+
+  const int r = lane & 15, kb = lane >> 4;
   const uint4* wl = wpk + lane;              // [tap][64 lanes]: lane's 16 B of the tap's B fragment
   uint32_t zoff[KS];                         // byte offset of (hz = r + dz, chunk kb) within a halo row
 #pragma unroll
   for (int dz = 0; dz < KS; ++dz) zoff[dz] = uint32_t(((r + dz) * 4 + (kb ^ swz(r + dz))) * 16);
-  // Software pipeline over the 49 (dx, dy) rows of taps.  With one wave per SIMD (the halo
-  // fills the LDS) nothing else hides latency, so while row i's 28 MFMAs run, row i+1's 28
-  // A fragments (LDS) and 7 B fragments (L2) are already in flight: 2 x 140 VGPRs of
-  // operands, affordable at one wave per SIMD.
-  uint4 acur[KS][TY], anxt[KS][TY], bcur[KS], bnxt[KS];
-  auto load_row = [&](int rowi, uint4 (&a)[KS][TY], uint4 (&bf)[KS]) {
-    const int dx = rowi / KS, dy = rowi - dx * KS;
-    const char* hb = reinterpret_cast<const char*>(halo) + uint32_t(((w + dx) * HY + dy) * HZ * 64);
-#pragma unroll
-    for (int dz = 0; dz < KS; ++dz) {
-      bf[dz] = wl[(rowi * KS + dz) * kWave];
-#pragma unroll
-      for (int m = 0; m < TY; ++m) a[dz][m] = *reinterpret_cast<const uint4*>(hb + zoff[dz] + m * HZ * 64);
-    }
-  };
-  auto mma_row = [&](const uint4 (&a)[KS][TY], const uint4 (&bf)[KS]) {
-#pragma unroll
-    for (int dz = 0; dz < KS; ++dz)
-#pragma unroll
-      for (int m = 0; m < TY; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[dz][m]),
-                                                         __builtin_bit_cast(bf16x8_t, bf[dz]), acc[m], 0, 0, 0);
-  };
-  load_row(0, acur, bcur);
-  for (int rowi = 0; rowi < KS * KS; rowi += 2) {
-    if (rowi + 1 < KS * KS) load_row(rowi + 1, anxt, bnxt);
-    __builtin_amdgcn_sched_barrier(0);
-    mma_row(acur, bcur);
-    __builtin_amdgcn_sched_barrier(0);
-    if (rowi + 1 >= KS * KS) break;
-    if (rowi + 2 < KS * KS) load_row(rowi + 2, acur, bcur);
-    __builtin_amdgcn_sched_barrier(0);
-    mma_row(anxt, bnxt);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-
-  // ---- epilogue: folded BN + ReLU, 4 consecutive z of one output channel per lane ----
   const int co = lane & 15, zr = (lane >> 4) * 4;
   const float s = scale[co], sh = shift[co];
+
+  load_slices(-PAD, HX);
+  for (int tx = 0; tx < nTx; ++tx) {
+    __syncthreads();                          // the tile's slices are in LDS
+    const int x0 = tx * TX;
+    f32x4_t acc[TY];
 #pragma unroll
-  for (int m = 0; m < TY; ++m) {
-    float y[4];
+    for (int m = 0; m < TY; ++m) acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // Software pipeline over the 49 (dx, dy) rows of taps.  With one wave per SIMD (the
+    // halo fills the LDS) nothing else hides latency, so while row i's 28 MFMAs run, row
+    // i+1's 28 A fragments (LDS) and 7 B fragments (L2) are already in flight.
+    uint4 acur[KS][TY], anxt[KS][TY], bcur[KS], bnxt[KS];
+    auto load_row = [&](int rowi, uint4 (&a)[KS][TY], uint4 (&bf)[KS]) {
+      const int dx = rowi / KS, dy = rowi - dx * KS;
+      const int slot = (x0 + w + dx) % HX;                  // halo x = w + dx  <->  gx = x0 - PAD + w + dx
+      const char* hb = reinterpret_cast<const char*>(halo) + uint32_t((slot * HY + dy) * HZ * 64);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) y[i] = fmaxf(__builtin_fmaf(acc[m][i], s, sh), 0.f);
-    TO* o = out + (((size_t(b) * CO + co) * V + (x0 + w)) * V + (y0 + m)) * V + z0 + zr;
-    if constexpr (sizeof(TO) == 4) {
-      *reinterpret_cast<float4*>(o) = make_float4(y[0], y[1], y[2], y[3]);
-    } else {
-      *reinterpret_cast<uint2*>(o) = make_uint2(pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3]));
+      for (int dz = 0; dz < KS; ++dz) {
+        bf[dz] = wl[(rowi * KS + dz) * kWave];
+#pragma unroll
+        for (int m = 0; m < TY; ++m) a[dz][m] = *reinterpret_cast<const uint4*>(hb + zoff[dz] + m * HZ * 64);
+      }
+    };
+    auto mma_row = [&](const uint4 (&a)[KS][TY], const uint4 (&bf)[KS]) {
+#pragma unroll
+      for (int dz = 0; dz < KS; ++dz)
+#pragma unroll
+        for (int m = 0; m < TY; ++m)
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[dz][m]),
+                                                           __builtin_bit_cast(bf16x8_t, bf[dz]), acc[m], 0, 0, 0);
+    };
+    load_row(0, acur, bcur);
+    for (int rowi = 0; rowi < KS * KS; rowi += 2) {
+      if (rowi + 1 < KS * KS) load_row(rowi + 1, anxt, bnxt);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_row(acur, bcur);
+      __builtin_amdgcn_sched_barrier(0);
+      if (rowi + 1 >= KS * KS) break;
+      if (rowi + 2 < KS * KS) load_row(rowi + 2, acur, bcur);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_row(anxt, bnxt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();                          // every wave is done with slices x0-3 .. x0
+    if (tx + 1 < nTx) load_slices(x0 + TX + HX - TX - PAD, TX);   // gx = x0+7 .. x0+10
+
+    // ---- epilogue: folded BN + ReLU, 4 consecutive z of one output channel per lane ----
+#pragma unroll
+    for (int m = 0; m < TY; ++m) {
+      float y[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[i] = fmaxf(__builtin_fmaf(acc[m][i], s, sh), 0.f);
+      TO* o = out + (((size_t(b) * CO + co) * V + (x0 + w)) * V + (y0 + m)) * V + z0 + zr;
+      if constexpr (sizeof(TO) == 4) {
+        *reinterpret_cast<float4*>(o) = make_float4(y[0], y[1], y[2], y[3]);
+      } else {
+        *reinterpret_cast<uint2*>(o) = make_uint2(pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3]));
+      }
     }
   }
 }
@@ -170,7 +180,7 @@ extern "C" int mvn_v2v_front(const void* vol_cl, const void* weight_packed, cons
   if (!vol_cl || !weight_packed || !scale || !shift || !out) return MVN_ERR_ARG;
   if (B <= 0 || V <= 0 || V % TZ != 0 || V % TX != 0 || V % TY != 0) return MVN_ERR_SHAPE;
   if ((long long)V * V * V * CI * 2 >= (1LL << 31)) return MVN_ERR_SHAPE;
-  const long long nblk = (long long)B * (V / TX) * (V / TY) * (V / TZ);
+  const long long nblk = (long long)B * (V / TY) * (V / TZ);       // one block per tile column along x
   if (nblk > INT_MAX) return MVN_ERR_SHAPE;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const auto* in = static_cast<const uint16_t*>(vol_cl);

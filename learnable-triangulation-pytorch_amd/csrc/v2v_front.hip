@@ -19,6 +19,8 @@
 // Arithmetic: 2 * 32 * 16 * 343 * V^3 flop per frame (92.1 GFLOP at V = 64): MFMA-bound.
 #include <climits>
 
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace mvn {
@@ -115,41 +117,64 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
     f32x4_t acc[TY];
 #pragma unroll
     for (int m = 0; m < TY; ++m) acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    // Software pipeline over the 49 (dx, dy) rows of taps.  With one wave per SIMD (the
-    // halo fills the LDS) nothing else hides latency, so while row i's 28 MFMAs run, row
-    // i+1's 28 A fragments (LDS) and 7 B fragments (L2) are already in flight.
-    uint4 acur[KS][TY], anxt[KS][TY], bcur[KS], bnxt[KS];
-    auto load_row = [&](int rowi, uint4 (&a)[KS][TY], uint4 (&bf)[KS]) {
-      const int dx = rowi / KS, dy = rowi - dx * KS;
+    // Register reuse of the A operand: tap (dx, dy, dz) of output row m reads halo y-row
+    // hy = dy + m, so for a fixed dx the 4 accumulators share 10 halo rows.  The rows live in
+    // a 5-slot register ring (slot hy % 5; 10 rows per dx keep the mapping across dx) and
+    // each is read from LDS once per dx: 70 ds_read_b128 per dx instead of 196, which takes
+    // the LDS array (4 cycles per read per wave, 4 waves per CU) off the critical path of
+    // the 16-cycle MFMA.  Step dy runs taps (dx, dy, *) on rows dy..dy+3 (one accumulation
+    // chain per row, full rate on 16x16x32); a row is loaded 28 MFMAs before it is first
+    // used — at the start of step dy - 4, or, across a dx boundary, as soon as the last step
+    // of the previous dx frees its slot.  B (7 fragments per tap row, from L2) is a 2-slot
+    // ring one step ahead; its parity flips every dx (7 steps), hence the P template.
+    uint4 A[5][KS], Bw[2][KS];
+    const char* hbase = reinterpret_cast<const char*>(halo);
+    auto lds_row = [&](int dx, int hy, uint4 (&dst)[KS]) {
       const int slot = (x0 + w + dx) % HX;                  // halo x = w + dx  <->  gx = x0 - PAD + w + dx
-      const char* hb = reinterpret_cast<const char*>(halo) + uint32_t((slot * HY + dy) * HZ * 64);
+      const char* hb = hbase + uint32_t((slot * HY + hy) * HZ * 64);
 #pragma unroll
-      for (int dz = 0; dz < KS; ++dz) {
-        bf[dz] = wl[(rowi * KS + dz) * kWave];
+      for (int dz = 0; dz < KS; ++dz) dst[dz] = *reinterpret_cast<const uint4*>(hb + zoff[dz]);
+    };
+    auto ld_b = [&](int dx, int dy, uint4 (&dst)[KS]) {
 #pragma unroll
-        for (int m = 0; m < TY; ++m) a[dz][m] = *reinterpret_cast<const uint4*>(hb + zoff[dz] + m * HZ * 64);
+      for (int dz = 0; dz < KS; ++dz) dst[dz] = wl[((dx * KS + dy) * KS + dz) * kWave];
+    };
+    auto dx_body = [&](int dx, auto parity) {
+      constexpr int P = decltype(parity)::value;
+      const bool more = dx + 1 < KS;
+#pragma unroll
+      for (int dy = 0; dy < KS; ++dy) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (dy + 1 < KS) {
+          lds_row(dx, dy + 4, A[(dy + 4) % 5]);
+          ld_b(dx, dy + 1, Bw[(dy + 1 + P) & 1]);
+        } else if (more) {
+          lds_row(dx + 1, 0, A[0]);
+          ld_b(dx + 1, 0, Bw[(KS + P) & 1]);
+        }
+#pragma unroll
+        for (int m = 0; m < TY; ++m) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int dz = 0; dz < KS; ++dz)
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, A[(dy + m) % 5][dz]),
+                                                             __builtin_bit_cast(bf16x8_t, Bw[(dy + P) & 1][dz]),
+                                                             acc[m], 0, 0, 0);
+          if (dy + 1 == KS && more && m + 1 < TY) {         // rows 1..3 of dx + 1 into the freed slots
+            __builtin_amdgcn_sched_barrier(0);
+            lds_row(dx + 1, m + 1, A[m + 1]);
+          }
+        }
       }
     };
-    auto mma_row = [&](const uint4 (&a)[KS][TY], const uint4 (&bf)[KS]) {
 #pragma unroll
-      for (int dz = 0; dz < KS; ++dz)
-#pragma unroll
-        for (int m = 0; m < TY; ++m)
-          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[dz][m]),
-                                                           __builtin_bit_cast(bf16x8_t, bf[dz]), acc[m], 0, 0, 0);
-    };
-    load_row(0, acur, bcur);
-    for (int rowi = 0; rowi < KS * KS; rowi += 2) {
-      if (rowi + 1 < KS * KS) load_row(rowi + 1, anxt, bnxt);
-      __builtin_amdgcn_sched_barrier(0);
-      mma_row(acur, bcur);
-      __builtin_amdgcn_sched_barrier(0);
-      if (rowi + 1 >= KS * KS) break;
-      if (rowi + 2 < KS * KS) load_row(rowi + 2, acur, bcur);
-      __builtin_amdgcn_sched_barrier(0);
-      mma_row(anxt, bnxt);
-      __builtin_amdgcn_sched_barrier(0);
+    for (int hy = 0; hy < TY; ++hy) lds_row(0, hy, A[hy]);
+    ld_b(0, 0, Bw[0]);
+    for (int dx = 0; dx < KS; dx += 2) {
+      dx_body(dx, std::integral_constant<int, 0>{});
+      if (dx + 1 < KS) dx_body(dx + 1, std::integral_constant<int, 1>{});
     }
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();                          // every wave is done with slices x0-3 .. x0
     if (tx + 1 < nTx) load_slices(x0 + TX + HX - TX - PAD, TX);   // gx = x0+7 .. x0+10
 

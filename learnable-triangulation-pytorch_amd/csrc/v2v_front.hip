@@ -9,16 +9,15 @@
 //
 // Implicit GEMM, one MFMA per (16 output voxels, tap): A = 16 z-consecutive voxels x 32
 // input channels (the tap-shifted input, read from an LDS halo), B = the tap's 32 x 16
-// weights (prepacked [tap][cout][cin], straight from L2 into registers, one 7-tap row ahead),
-// C = 16 voxels x 16 output channels in f32.  A block walks a column of 4 x 4 x 16 output
-// tiles along x: the 10 x 10 x 22-voxel input halo (140,800 B of LDS, zero-padded at the
-// volume border like Conv3d's padding=3) is a ring of x-slices, 4 new slices per tile; each
-// of the 4 waves takes one x-row of the tile (4 M-blocks = 4 accumulators) and walks the
-// 343 taps.  Per tap and wave: 1 global 16-B
-// weight load and 4 x (ds_read_b128 + v_mfma_f32_16x16x32_bf16).
+// weights (prepacked [tap][lane][8], straight from L2 into registers), C = 16 voxels x 16
+// output channels in f32.  A block walks a column of 4 x 4 x 16 output tiles along x: the
+// 10 x 10 x 22-voxel input halo (140,800 B of LDS, zero-padded at the volume border like
+// Conv3d's padding=3) is a ring of x-slices, 4 new slices per tile.  4 waves, one per SIMD,
+// each computing the whole 4 x 4 x 16 tile (16 accumulators, so every B fragment feeds 16
+// MFMAs) over a quarter of the 49 (dx, dz) tap passes (12 each, and the 49th split by
+// output x-row); the partial sums meet in the tile's dead halo slots.
 // Arithmetic: 2 * 32 * 16 * 343 * V^3 flop per frame (92.1 GFLOP at V = 64): MFMA-bound.
 #include <climits>
-
 #include <type_traits>
 
 #include "common.hpp"
@@ -30,12 +29,12 @@ constexpr int CI = 32, CO = 16, KS = 7, PAD = 3, NTAP = KS * KS * KS;
 constexpr int TX = 4, TY = 4, TZ = 16;
 constexpr int HX = TX + KS - 1, HY = TY + KS - 1, HZ = TZ + KS - 1;   // 10, 10, 22
 constexpr int HVOX = HX * HY * HZ;                                     // 2200 voxels, 64 B each
-constexpr int kThreads = 256;
+constexpr int kWaves = 4, kThreads = kWaves * kWave;
+constexpr int kPass = KS * KS;                                         // (dx, dz) tap passes
 constexpr uint32_t kOob = 0x80000000u;
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
@@ -54,11 +53,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 __device__ __forceinline__ int swz(int hz) { return ((hz >> 2) & 1) << 1; }
 
 template <typename TO>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void v2v_front(const uint16_t* __restrict__ in, const uint4* __restrict__ wpk,
-                                                     const float* __restrict__ scale, const float* __restrict__ shift,
-                                                     TO* __restrict__ out, int V) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void v2v_front(
+    const uint16_t* __restrict__ in, const uint4* __restrict__ wpk, const float* __restrict__ scale,
+    const float* __restrict__ shift, TO* __restrict__ out, int V) {
   __shared__ uint4 halo[HVOX * 4];          // ring of HX x-slices: [slot][hy][hz][8-channel chunk]
-  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const int t = threadIdx.x, lane = t & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(t / kWave);
   const int nTz = V / TZ, nTy = V / TY, nTx = V / TX;
   // A block walks one column of tiles along x (nTx tiles): consecutive tiles' halos share
   // HX - TX = 6 of their 10 x-slices, so per tile only TX = 4 new slices are loaded into a
@@ -71,119 +71,208 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
   const size_t nvox = size_t(V) * V * V;
   const __amdgpu_buffer_rsrc_t irs = make_rsrc(in + size_t(b) * nvox * CI, uint32_t(nvox * CI * 2));
   constexpr int kSliceChunks = HY * HZ * 4;                  // 880 chunks of 16 B per x-slice
+  constexpr int kSlotBytes = kSliceChunks * 16;              // 14,080 B
+  constexpr int kStage = (TX * kSliceChunks + kThreads - 1) / kThreads;   // 14 chunks per thread per tile
 
-  // load x-slices gx0 .. gx0 + n - 1 (zero outside the volume) into their ring slots;
-  // batches of 14 loads per thread in flight before the LDS writes
-  auto load_slices = [&](int gx0, int n) {
-    const int total = n * kSliceChunks;
-    constexpr int kBatch = 14;
+  // halo chunk q of the slices gx0, gx0 + 1, ...: its global byte offset (kOob: zero,
+  // outside the volume or past the last chunk) and its LDS index in the ring
+  auto chunk_src = [&](int gx0, int q, int total) -> uint32_t {
+    const int sl = q / kSliceChunks, rem = q - sl * kSliceChunks;
+    const int v = rem >> 2, c = rem & 3;
+    const int hz = v % HZ, hy = v / HZ;
+    const int gx = gx0 + sl, gy = y0 + hy - PAD, gz = z0 + hz - PAD;
+    const bool ok = (q < total) & (unsigned(gx) < unsigned(V)) & (unsigned(gy) < unsigned(V)) &
+                    (unsigned(gz) < unsigned(V));
+    return ok ? uint32_t(((size_t(gx) * V + gy) * V + gz) * CI * 2 + c * 16) : kOob;
+  };
+  auto chunk_dst = [&](int gx0, int q) -> int {
+    const int sl = q / kSliceChunks, rem = q - sl * kSliceChunks;
+    const int v = rem >> 2, c = rem & 3;
+    const int hz = v % HZ;
+    return ((gx0 + sl + PAD) % HX) * kSliceChunks + v * 4 + (c ^ swz(hz));
+  };
+  auto ld_chunk = [&](uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(irs, off, 0, 0));
+  };
+  {  // the first tile's 10 slices
+    constexpr int kBatch = 7, total = HX * kSliceChunks;
     for (int i0 = 0; i0 * kThreads < total; i0 += kBatch) {
       uint4 vals[kBatch];
-      int dst[kBatch];
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) vals[u] = ld_chunk(chunk_src(-PAD, t + (i0 + u) * kThreads, total));
 #pragma unroll
       for (int u = 0; u < kBatch; ++u) {
         const int q = t + (i0 + u) * kThreads;
-        dst[u] = -1;
-        if (q < total) {
-          const int sl = q / kSliceChunks, rem = q - sl * kSliceChunks;
-          const int v = rem >> 2, c = rem & 3;
-          const int hz = v % HZ, hy = v / HZ;
-          const int gx = gx0 + sl, gy = y0 + hy - PAD, gz = z0 + hz - PAD;
-          const bool ok = (unsigned(gx) < unsigned(V)) & (unsigned(gy) < unsigned(V)) & (unsigned(gz) < unsigned(V));
-          const uint32_t off = ok ? uint32_t(((size_t(gx) * V + gy) * V + gz) * CI * 2 + c * 16) : kOob;
-          vals[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(irs, off, 0, 0));
-          const int slot = (gx + PAD) % HX;
-          dst[u] = slot * kSliceChunks + v * 4 + (c ^ swz(hz));
-        }
+        if (q < total) halo[chunk_dst(-PAD, q)] = vals[u];
       }
-#pragma unroll
-      for (int u = 0; u < kBatch; ++u)
-        if (dst[u] >= 0) halo[dst[u]] = vals[u];
     }
-  };
+  }
 
   const int r = lane & 15, kb = lane >> 4;
-  const uint4* wl = wpk + lane;              // [tap][64 lanes]: lane's 16 B of the tap's B fragment
-  uint32_t zoff[KS];                         // byte offset of (hz = r + dz, chunk kb) within a halo row
-#pragma unroll
-  for (int dz = 0; dz < KS; ++dz) zoff[dz] = uint32_t(((r + dz) * 4 + (kb ^ swz(r + dz))) * 16);
+  // packed weights [tap][64 lanes][16 B]: lane offset in a VGPR, tap offset in an SGPR
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(wpk, uint32_t(NTAP * kWave * 16));
+  const int lane16 = lane * 16;
   const int co = lane & 15, zr = (lane >> 4) * 4;
   const float s = scale[co], sh = shift[co];
+  const char* hbase = reinterpret_cast<const char*>(halo);
+  constexpr int kCommon = (kPass - 1) / kWaves;              // 12 whole passes per wave; pass 48 split by x-row
+  const int p0 = w * kCommon;
 
-  load_slices(-PAD, HX);
   for (int tx = 0; tx < nTx; ++tx) {
     __syncthreads();                          // the tile's slices are in LDS
     const int x0 = tx * TX;
-    f32x4_t acc[TY];
+    const bool more = tx + 1 < nTx;
+    const int gxn = x0 + TX + HX - TX - PAD;  // next tile's new slices: gx = x0+7 .. x0+10
+    f32x4_t acc[TX][TY];
 #pragma unroll
-    for (int m = 0; m < TY; ++m) acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    // Register reuse of the A operand: tap (dx, dy, dz) of output row m reads halo y-row
-    // hy = dy + m, so for a fixed dx the 4 accumulators share 10 halo rows.  The rows live in
-    // a 5-slot register ring (slot hy % 5; 10 rows per dx keep the mapping across dx) and
-    // each is read from LDS once per dx: 70 ds_read_b128 per dx instead of 196, which takes
-    // the LDS array (4 cycles per read per wave, 4 waves per CU) off the critical path of
-    // the 16-cycle MFMA.  Step dy runs taps (dx, dy, *) on rows dy..dy+3 (one accumulation
-    // chain per row, full rate on 16x16x32); a row is loaded 28 MFMAs before it is first
-    // used — at the start of step dy - 4, or, across a dx boundary, as soon as the last step
-    // of the previous dx frees its slot.  B (7 fragments per tap row, from L2) is a 2-slot
-    // ring one step ahead; its parity flips every dx (7 steps), hence the P template.
-    uint4 A[5][KS], Bw[2][KS];
-    const char* hbase = reinterpret_cast<const char*>(halo);
-    auto lds_row = [&](int dx, int hy, uint4 (&dst)[KS]) {
-      const int slot = (x0 + w + dx) % HX;                  // halo x = w + dx  <->  gx = x0 - PAD + w + dx
-      const char* hb = hbase + uint32_t((slot * HY + hy) * HZ * 64);
+    for (int x = 0; x < TX; ++x)
 #pragma unroll
-      for (int dz = 0; dz < KS; ++dz) dst[dz] = *reinterpret_cast<const uint4*>(hb + zoff[dz]);
+      for (int m = 0; m < TY; ++m) acc[x][m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // Pass (dx, dz): for each output x-row x the 10 halo y-rows at halo x = x + dx, z offset
+    // dz (40 ds_read_b128) and the 7 taps (dx, 0..6, dz) (7 buffer loads); output (x, m)
+    // takes tap dy from halo row hy = dy + m: 112 MFMAs per pass, each A fragment used for
+    // up to 4 of them, each B fragment for 16 (B from L2 is 1/16 of a load per MFMA).  Step
+    // hy of a pass runs the MFMAs of halo row hy, after which A[.][hy] and B[hy - 3] are
+    // dead: the next pass's fragments are loaded into them right there, one pass ahead of
+    // use, with one register set.  The passes are unrolled into straight-line code: at a
+    // loop back-edge the compiler drains every load (more LDS reads are in flight than
+    // lgkmcnt counts) and shuffles accumulators.
+    uint4 A[TX][HY], Bf[KS];
+    auto a_addr = [&](int q, int x) {
+      const int dx = q / KS, dz = q - dx * KS;
+      int slot = (x0 + dx) % HX + x;                        // halo x = dx + x  <->  gx = x0 - PAD + dx + x
+      if (slot >= HX) slot -= HX;
+      return hbase + uint32_t(slot * HY * HZ * 64 + ((r + dz) * 4 + (kb ^ swz(r + dz))) * 16);
     };
-    auto ld_b = [&](int dx, int dy, uint4 (&dst)[KS]) {
-#pragma unroll
-      for (int dz = 0; dz < KS; ++dz) dst[dz] = wl[((dx * KS + dy) * KS + dz) * kWave];
+    auto b_off = [&](int q) {
+      const int dx = q / KS, dz = q - dx * KS;
+      return __builtin_amdgcn_readfirstlane((dx * KS * KS + dz) * kWave * 16);   // tap (dx, 0, dz), bytes
     };
-    auto dx_body = [&](int dx, auto parity) {
-      constexpr int P = decltype(parity)::value;
-      const bool more = dx + 1 < KS;
+    auto ld_a = [&](const char* hb, int hy) { return *reinterpret_cast<const uint4*>(hb + hy * HZ * 64); };
+    auto ld_b = [&](int wq, int dy) {
+      return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane16, wq + dy * KS * kWave * 16, 0));
+    };
+    // run the pass held in A / Bf (all x-rows, or x-row XONLY into slot 0) and load pass qn
+    // (all x-rows, or only x-row w into slot 0 when NEXT_ONE)
+    auto pass = [&](int qn, auto next_one, auto xonly) {
+      constexpr bool NEXT_ONE = decltype(next_one)::value;
+      constexpr int XONLY = decltype(xonly)::value;
+      const int wq = b_off(qn);
+      const char* hb[TX];
 #pragma unroll
-      for (int dy = 0; dy < KS; ++dy) {
+      for (int x = 0; x < TX; ++x) hb[x] = a_addr(qn, NEXT_ONE ? w : x);
+#pragma unroll
+      for (int hy = 0; hy < HY; ++hy) {
         __builtin_amdgcn_sched_barrier(0);
-        if (dy + 1 < KS) {
-          lds_row(dx, dy + 4, A[(dy + 4) % 5]);
-          ld_b(dx, dy + 1, Bw[(dy + 1 + P) & 1]);
-        } else if (more) {
-          lds_row(dx + 1, 0, A[0]);
-          ld_b(dx + 1, 0, Bw[(KS + P) & 1]);
-        }
 #pragma unroll
         for (int m = 0; m < TY; ++m) {
-          __builtin_amdgcn_sched_barrier(0);
+          const int dy = hy - m;
+          if (dy >= 0 && dy < KS) {
+            if constexpr (XONLY < 0) {
 #pragma unroll
-          for (int dz = 0; dz < KS; ++dz)
-            acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, A[(dy + m) % 5][dz]),
-                                                             __builtin_bit_cast(bf16x8_t, Bw[(dy + P) & 1][dz]),
-                                                             acc[m], 0, 0, 0);
-          if (dy + 1 == KS && more && m + 1 < TY) {         // rows 1..3 of dx + 1 into the freed slots
-            __builtin_amdgcn_sched_barrier(0);
-            lds_row(dx + 1, m + 1, A[m + 1]);
+              for (int x = 0; x < TX; ++x)
+                acc[x][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, A[x][hy]),
+                                                                    __builtin_bit_cast(bf16x8_t, Bf[dy]), acc[x][m], 0, 0, 0);
+            } else {
+              acc[XONLY][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, A[0][hy]),
+                                                                      __builtin_bit_cast(bf16x8_t, Bf[dy]), acc[XONLY][m], 0, 0, 0);
+            }
           }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (qn >= 0) {
+#pragma unroll
+          for (int x = 0; x < (NEXT_ONE ? 1 : TX); ++x) A[x][hy] = ld_a(hb[x], hy);
+          if (hy >= TY - 1) Bf[hy - (TY - 1)] = ld_b(wq, hy - (TY - 1));
         }
       }
     };
+    using F = std::false_type;
+    using T = std::true_type;
+    using ALLX = std::integral_constant<int, -1>;
+    {  // first pass of this wave
+      const int wq = b_off(p0);
 #pragma unroll
-    for (int hy = 0; hy < TY; ++hy) lds_row(0, hy, A[hy]);
-    ld_b(0, 0, Bw[0]);
-    for (int dx = 0; dx < KS; dx += 2) {
-      dx_body(dx, std::integral_constant<int, 0>{});
-      if (dx + 1 < KS) dx_body(dx + 1, std::integral_constant<int, 1>{});
+      for (int i = 0; i < KS; ++i) Bf[i] = ld_b(wq, i);
+#pragma unroll
+      for (int x = 0; x < TX; ++x) {
+        const char* hb = a_addr(p0, x);
+#pragma unroll
+        for (int i = 0; i < HY; ++i) A[x][i] = ld_a(hb, i);
+      }
+    }
+    // the next tile's 4 new slices: loaded into registers during the passes, written to LDS
+    // once every wave is done with the slots they replace
+    uint4 sv[kStage];
+#pragma unroll
+    for (int i = 0; i < kCommon; ++i) {
+      if (i + 1 < kCommon) pass(p0 + i + 1, F{}, ALLX{});
+      else pass(kPass - 1, T{}, ALLX{});                   // then pass 48, own x-row only
+      if (i < (kStage + 1) / 2) {
+#pragma unroll
+        for (int u = 2 * i; u < 2 * i + 2 && u < kStage; ++u)
+          sv[u] = ld_chunk(more ? chunk_src(gxn, t + u * kThreads, TX * kSliceChunks) : kOob);
+      }
+    }
+    switch (w) {
+      case 0: pass(-1, T{}, std::integral_constant<int, 0>{}); break;
+      case 1: pass(-1, T{}, std::integral_constant<int, 1>{}); break;
+      case 2: pass(-1, T{}, std::integral_constant<int, 2>{}); break;
+      default: pass(-1, T{}, std::integral_constant<int, 3>{}); break;
     }
     __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();                          // every wave is done with slices x0-3 .. x0
-    if (tx + 1 < nTx) load_slices(x0 + TX + HX - TX - PAD, TX);   // gx = x0+7 .. x0+10
+
+    // ---- partial sums: wave k owns output x-row k.  The 4 slots of slices x0-3 .. x0 are
+    // dead now (they take the next tile's slices): each wave writes its partials of the 3
+    // x-rows it does not own there ([owner][source][m][lane] f32x4, 48 KiB), then sums its own.
+    const int s0 = x0 % HX;
+    auto red_addr = [&](int owner, int j, int m) {
+      const int o = (((owner * (kWaves - 1) + j) * TY + m) * kWave + lane) * 16;
+      const int sl = o / kSlotBytes;
+      int slot = s0 + sl;
+      if (slot >= HX) slot -= HX;
+      return reinterpret_cast<f32x4_t*>(const_cast<char*>(hbase) + slot * kSlotBytes + (o - sl * kSlotBytes));
+    };
+    __syncthreads();                          // every wave is done with the halo
+#pragma unroll
+    for (int k = 0; k < TX; ++k)
+      if (k != w) {
+        const int j = w < k ? w : w - 1;
+#pragma unroll
+        for (int m = 0; m < TY; ++m) *red_addr(k, j, m) = acc[k][m];
+      }
+    __syncthreads();
+    f32x4_t sum[TY];
+    auto gather = [&](auto own) {
+      constexpr int K = decltype(own)::value;
+#pragma unroll
+      for (int m = 0; m < TY; ++m) {
+        sum[m] = acc[K][m];
+#pragma unroll
+        for (int j = 0; j < kWaves - 1; ++j) sum[m] += *red_addr(K, j, m);
+      }
+    };
+    switch (w) {
+      case 0: gather(std::integral_constant<int, 0>{}); break;
+      case 1: gather(std::integral_constant<int, 1>{}); break;
+      case 2: gather(std::integral_constant<int, 2>{}); break;
+      default: gather(std::integral_constant<int, 3>{}); break;
+    }
+    __syncthreads();                          // the dead slots are read: the next slices go in
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < kStage; ++u) {
+        const int q = t + u * kThreads;
+        if (q < TX * kSliceChunks) halo[chunk_dst(gxn, q)] = sv[u];
+      }
+    }
 
     // ---- epilogue: folded BN + ReLU, 4 consecutive z of one output channel per lane ----
 #pragma unroll
     for (int m = 0; m < TY; ++m) {
       float y[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) y[i] = fmaxf(__builtin_fmaf(acc[m][i], s, sh), 0.f);
+      for (int i = 0; i < 4; ++i) y[i] = fmaxf(__builtin_fmaf(sum[m][i], s, sh), 0.f);
       TO* o = out + (((size_t(b) * CO + co) * V + (x0 + w)) * V + (y0 + m)) * V + z0 + zr;
       if constexpr (sizeof(TO) == 4) {
         *reinterpret_cast<float4*>(o) = make_float4(y[0], y[1], y[2], y[3]);

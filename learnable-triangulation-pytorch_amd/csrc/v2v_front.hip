@@ -31,6 +31,9 @@ constexpr int HX = TX + KS - 1, HY = TY + KS - 1, HZ = TZ + KS - 1;   // 10, 10,
 constexpr int HVOX = HX * HY * HZ;                                     // 2200 voxels, 64 B each
 constexpr int kWaves = 4, kThreads = kWaves * kWave;
 constexpr int kPass = KS * KS;                                         // (dx, dz) tap passes
+constexpr int kStage = (TX * HY * HZ * 4 + kThreads - 1) / kThreads;   // halo chunks per thread per tile: 14
+// __builtin_amdgcn_sched_group_barrier instruction classes
+constexpr int kSgMfma = 0x008, kSgVmemRead = 0x020, kSgDsRead = 0x100;
 constexpr uint32_t kOob = 0x80000000u;
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -72,10 +75,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
   const __amdgpu_buffer_rsrc_t irs = make_rsrc(in + size_t(b) * nvox * CI, uint32_t(nvox * CI * 2));
   constexpr int kSliceChunks = HY * HZ * 4;                  // 880 chunks of 16 B per x-slice
   constexpr int kSlotBytes = kSliceChunks * 16;              // 14,080 B
-  constexpr int kStage = (TX * kSliceChunks + kThreads - 1) / kThreads;   // 14 chunks per thread per tile
 
   // halo chunk q of the slices gx0, gx0 + 1, ...: its global byte offset (kOob: zero,
   // outside the volume or past the last chunk) and its LDS index in the ring
+  static_assert((kWaves - 1) * TY * kWave * 16 <= kSlotBytes, "partial-sum blocks must fit a halo slot");
   auto chunk_src = [&](int gx0, int q, int total) -> uint32_t {
     const int sl = q / kSliceChunks, rem = q - sl * kSliceChunks;
     const int v = rem >> 2, c = rem & 3;
@@ -108,6 +111,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
   }
 
+  // Per-tile staging of chunk q = t + u * kThreads (u < kStage) of the 4 new slices: the
+  // in-slice part is tile-invariant, so it is decoded once into a packed descriptor:
+  // bit 0 valid (q in range), bits 1-2 slice, bits 3-12 LDS index within the slot,
+  // bit 13 y/z inside the volume, bits 14-31 (gy * V + gz) * 4 + c (V <= 256).
+  uint32_t sdesc[kStage];
+#pragma unroll
+  for (int u = 0; u < kStage; ++u) {
+    const int q = t + u * kThreads;
+    const int sl = q / kSliceChunks, rem = q - sl * kSliceChunks;
+    const int v = rem >> 2, c = rem & 3;
+    const int hz = v % HZ, hy = v / HZ;
+    const int gy = y0 + hy - PAD, gz = z0 + hz - PAD;
+    const bool yz = (unsigned(gy) < unsigned(V)) & (unsigned(gz) < unsigned(V));
+    sdesc[u] = (q < TX * kSliceChunks ? 1u : 0u) | (uint32_t(sl & 3) << 1) | (uint32_t(v * 4 + (c ^ swz(hz))) << 3) |
+               (yz ? (1u << 13) | (uint32_t((gy * V + gz) * 4 + c) << 14) : 0u);
+  }
+  auto stage_src = [&](int u, int gx0) -> uint32_t {
+    const uint32_t d = sdesc[u];
+    const int gx = gx0 + int((d >> 1) & 3u);
+    const bool ok = ((d & ((1u << 13) | 1u)) == ((1u << 13) | 1u)) & (unsigned(gx) < unsigned(V));
+    return ok ? uint32_t(gx) * uint32_t(V * V * CI * 2) + (d >> 14) * 16u : kOob;
+  };
+
   const int r = lane & 15, kb = lane >> 4;
   // packed weights [tap][64 lanes][16 B]: lane offset in a VGPR, tap offset in an SGPR
   const __amdgpu_buffer_rsrc_t wrs = make_rsrc(wpk, uint32_t(NTAP * kWave * 16));
@@ -117,6 +143,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
   const char* hbase = reinterpret_cast<const char*>(halo);
   constexpr int kCommon = (kPass - 1) / kWaves;              // 12 whole passes per wave; pass 48 split by x-row
   const int p0 = w * kCommon;
+
+  // B fragments: the 7 taps (dx, 0..6, dz) of a pass
+  uint4 Bf[KS];
+  auto ld_b = [&](int wq, int dy) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane16, wq + dy * KS * kWave * 16, 0));
+  };
+  auto b_off = [&](int q) {
+    const int dx = q / KS, dz = q - dx * KS;
+    return __builtin_amdgcn_readfirstlane((dx * KS * KS + dz) * kWave * 16);   // tap (dx, 0, dz), bytes
+  };
 
   for (int tx = 0; tx < nTx; ++tx) {
     __syncthreads();                          // the tile's slices are in LDS
@@ -137,54 +173,52 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
     // use, with one register set.  The passes are unrolled into straight-line code: at a
     // loop back-edge the compiler drains every load (more LDS reads are in flight than
     // lgkmcnt counts) and shuffles accumulators.
-    uint4 A[TX][HY], Bf[KS];
+    uint4 A[TX][HY];
     auto a_addr = [&](int q, int x) {
       const int dx = q / KS, dz = q - dx * KS;
       int slot = (x0 + dx) % HX + x;                        // halo x = dx + x  <->  gx = x0 - PAD + dx + x
       if (slot >= HX) slot -= HX;
       return hbase + uint32_t(slot * HY * HZ * 64 + ((r + dz) * 4 + (kb ^ swz(r + dz))) * 16);
     };
-    auto b_off = [&](int q) {
-      const int dx = q / KS, dz = q - dx * KS;
-      return __builtin_amdgcn_readfirstlane((dx * KS * KS + dz) * kWave * 16);   // tap (dx, 0, dz), bytes
-    };
     auto ld_a = [&](const char* hb, int hy) { return *reinterpret_cast<const uint4*>(hb + hy * HZ * 64); };
-    auto ld_b = [&](int wq, int dy) {
-      return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane16, wq + dy * KS * kWave * 16, 0));
-    };
     // run the pass held in A / Bf (all x-rows, or x-row XONLY into slot 0) and load pass qn
     // (all x-rows, or only x-row w into slot 0 when NEXT_ONE)
+    // run the pass held in A / Bf (all x-rows, or x-row XONLY in slot 0) and load pass qn
+    // (all x-rows, or only x-row w into slot 0 when NEXT_ONE; nothing when qn < 0)
     auto pass = [&](int qn, auto next_one, auto xonly) {
       constexpr bool NEXT_ONE = decltype(next_one)::value;
       constexpr int XONLY = decltype(xonly)::value;
-      const int wq = b_off(qn);
+      const int wq = b_off(qn < 0 ? 0 : qn);
       const char* hb[TX];
 #pragma unroll
-      for (int x = 0; x < TX; ++x) hb[x] = a_addr(qn, NEXT_ONE ? w : x);
+      for (int x = 0; x < TX; ++x) hb[x] = a_addr(qn < 0 ? 0 : qn, NEXT_ONE ? w : x);
 #pragma unroll
       for (int hy = 0; hy < HY; ++hy) {
         __builtin_amdgcn_sched_barrier(0);
+        const int m_lo = hy - (KS - 1) > 0 ? hy - (KS - 1) : 0, m_hi = hy < TY - 1 ? hy : TY - 1;
+        const int nm = m_hi - m_lo + 1;                       // MFMAs per x-row in this step
+        const bool la = qn >= 0, lb = qn >= 0 && hy >= TY - 1;
 #pragma unroll
-        for (int m = 0; m < TY; ++m) {
-          const int dy = hy - m;
-          if (dy >= 0 && dy < KS) {
-            if constexpr (XONLY < 0) {
+        for (int x = 0; x < TX; ++x) {
+          if (XONLY >= 0 && x > 0) break;
 #pragma unroll
-              for (int x = 0; x < TX; ++x)
-                acc[x][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, A[x][hy]),
-                                                                    __builtin_bit_cast(bf16x8_t, Bf[dy]), acc[x][m], 0, 0, 0);
-            } else {
-              acc[XONLY][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, A[0][hy]),
-                                                                      __builtin_bit_cast(bf16x8_t, Bf[dy]), acc[XONLY][m], 0, 0, 0);
-            }
+          for (int m = m_lo; m <= m_hi; ++m) {
+            const int xa = XONLY >= 0 ? XONLY : x;
+            acc[xa][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, A[x][hy]),
+                                                                 __builtin_bit_cast(bf16x8_t, Bf[hy - m]), acc[xa][m], 0, 0, 0);
           }
+          if (la && (!NEXT_ONE || x == 0)) A[x][hy] = ld_a(hb[x], hy);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        if (qn >= 0) {
+        if (lb) Bf[hy - (TY - 1)] = ld_b(wq, hy - (TY - 1));
+        // issue order: each x-row's MFMAs, then its A reload (one LDS read per MFMA group)
 #pragma unroll
-          for (int x = 0; x < (NEXT_ONE ? 1 : TX); ++x) A[x][hy] = ld_a(hb[x], hy);
-          if (hy >= TY - 1) Bf[hy - (TY - 1)] = ld_b(wq, hy - (TY - 1));
+        for (int x = 0; x < TX; ++x) {
+          if (XONLY >= 0 && x > 0) break;
+#pragma unroll
+          for (int i = 0; i < nm; ++i) __builtin_amdgcn_sched_group_barrier(kSgMfma, 1, 0);
+          if (la && (!NEXT_ONE || x == 0)) __builtin_amdgcn_sched_group_barrier(kSgDsRead, 1, 0);
         }
+        if (lb) __builtin_amdgcn_sched_group_barrier(kSgVmemRead, 1, 0);
       }
     };
     using F = std::false_type;
@@ -201,20 +235,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
         for (int i = 0; i < HY; ++i) A[x][i] = ld_a(hb, i);
       }
     }
-    // the next tile's 4 new slices: loaded into registers during the passes, written to LDS
-    // once every wave is done with the slots they replace
+    // the next tile's 4 new slices: loaded into registers during the passes (2 per pass),
+    // written to LDS once every wave is done with the slots they replace
     uint4 sv[kStage];
 #pragma unroll
     for (int i = 0; i < kCommon; ++i) {
       if (i + 1 < kCommon) pass(p0 + i + 1, F{}, ALLX{});
       else pass(kPass - 1, T{}, ALLX{});                   // then pass 48, own x-row only
-      if (i < (kStage + 1) / 2) {
+      if (2 * i < kStage) {
 #pragma unroll
-        for (int u = 2 * i; u < 2 * i + 2 && u < kStage; ++u)
-          sv[u] = ld_chunk(more ? chunk_src(gxn, t + u * kThreads, TX * kSliceChunks) : kOob);
+        for (int u = 2 * i; u < 2 * i + 2 && u < kStage; ++u) sv[u] = ld_chunk(more ? stage_src(u, gxn) : kOob);
       }
     }
-    switch (w) {
+    switch (w) {                              // pass 48, own x-row
       case 0: pass(-1, T{}, std::integral_constant<int, 0>{}); break;
       case 1: pass(-1, T{}, std::integral_constant<int, 1>{}); break;
       case 2: pass(-1, T{}, std::integral_constant<int, 2>{}); break;
@@ -224,14 +257,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
 
     // ---- partial sums: wave k owns output x-row k.  The 4 slots of slices x0-3 .. x0 are
     // dead now (they take the next tile's slices): each wave writes its partials of the 3
-    // x-rows it does not own there ([owner][source][m][lane] f32x4, 48 KiB), then sums its own.
+    // x-rows it does not own there — 4 KiB blocks [m][lane] f32x4, block (owner, source j)
+    // at slot owner, offset j * 4 KiB (3 blocks fit a 13.75 KiB slot) — then sums its own.
     const int s0 = x0 % HX;
     auto red_addr = [&](int owner, int j, int m) {
-      const int o = (((owner * (kWaves - 1) + j) * TY + m) * kWave + lane) * 16;
-      const int sl = o / kSlotBytes;
-      int slot = s0 + sl;
+      int slot = s0 + owner;
       if (slot >= HX) slot -= HX;
-      return reinterpret_cast<f32x4_t*>(const_cast<char*>(hbase) + slot * kSlotBytes + (o - sl * kSlotBytes));
+      return reinterpret_cast<f32x4_t*>(const_cast<char*>(hbase) + slot * kSlotBytes + j * (TY * kWave * 16) +
+                                        (m * kWave + lane) * 16);
     };
     __syncthreads();                          // every wave is done with the halo
 #pragma unroll
@@ -262,8 +295,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
     if (more) {
 #pragma unroll
       for (int u = 0; u < kStage; ++u) {
-        const int q = t + u * kThreads;
-        if (q < TX * kSliceChunks) halo[chunk_dst(gxn, q)] = sv[u];
+        const uint32_t d = sdesc[u];
+        if (d & 1u) {
+          int slot = ((gxn + PAD) % HX) + int((d >> 1) & 3u);
+          if (slot >= HX) slot -= HX;
+          halo[slot * kSliceChunks + int((d >> 3) & 1023u)] = sv[u];
+        }
       }
     }
 
@@ -292,7 +329,7 @@ extern "C" int mvn_v2v_front(const void* vol_cl, const void* weight_packed, cons
                              void* out, int out_dtype, int B, int V, void* stream) {
   using namespace mvn;
   if (!vol_cl || !weight_packed || !scale || !shift || !out) return MVN_ERR_ARG;
-  if (B <= 0 || V <= 0 || V % TZ != 0 || V % TX != 0 || V % TY != 0) return MVN_ERR_SHAPE;
+  if (B <= 0 || V <= 0 || V > 256 || V % TZ != 0 || V % TX != 0 || V % TY != 0) return MVN_ERR_SHAPE;
   if ((long long)V * V * V * CI * 2 >= (1LL << 31)) return MVN_ERR_SHAPE;
   const long long nblk = (long long)B * (V / TY) * (V / TZ);       // one block per tile column along x
   if (nblk > INT_MAX) return MVN_ERR_SHAPE;

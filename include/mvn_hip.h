@@ -146,7 +146,7 @@ int mvn_unproject_ex(const void* feat, int feat_dtype,
  *   weight_packed  mvn_v2v_front_packed_weight_bytes() bytes: bf16 weights as
  *                  [tap = (dx*7 + dy)*7 + dz][lane 0..63][j 0..7] = W[lane & 15][8*(lane >> 4) + j][dx][dy][dz]
  *   scale, shift   (16) f32: BN folded, y = relu(conv * scale + shift)
- *   out            (B, 16, V, V, V) out_dtype (f32 | bf16);  V % 16 == 0
+ *   out            (B, 16, V, V, V) out_dtype (f32 | bf16);  V % 16 == 0, V <= 256
  */
 size_t mvn_v2v_front_packed_weight_bytes(void);
 int mvn_v2v_front(const void* vol_cl, const void* weight_packed, const float* scale, const float* shift,

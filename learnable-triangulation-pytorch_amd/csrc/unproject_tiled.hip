@@ -52,7 +52,7 @@ constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any
 template <int NV> struct TileShape;
 // WAVES: waves per SIMD the register allocation must allow (4: two 512-thread blocks per CU).
 template <> struct TileShape<4> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, WAVES = 4; };
-template <> struct TileShape<8> { static constexpr int TX = 2, TY = 8, TZ = 16, THREADS = 256, SLOTS = 2048, WAVES = 2; };
+template <> struct TileShape<8> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 4096, WAVES = 2; };
 
 // Wave-wide integer min / max, returned wave-uniform.  row_shr DPP steps (identity
 // shifted in) leave each row's reduction in its lane 15; four readlanes combine the rows.
@@ -357,7 +357,7 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
   }
 
   // sample the views staged in an LDS buffer (ONE_PASS: all of them; else those of `pass`)
-  auto sample_views = [&](const char* buf, auto one_pass, int pass, float (&sv)[G][NV]) {
+  auto sample_views = [&](const char* buf, auto one_pass, int pass, float (&sv)[G][NV]) __attribute__((always_inline)) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (v >= N) continue;
@@ -378,7 +378,7 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
   // out_cl (channels-last (B, Vx, Vy, Vz, C) output, C % 4 == 0; the V2V front block's input
   // layout): one 16-byte (f32) / 8-byte (bf16) store of the group's 4 channels per voxel.
   const uint32_t ooff_cl = act ? uint32_t(vox) * uint32_t(C) * uint32_t(sizeof(TOut)) : kOob;
-  auto aggregate_store = [&](int c0, const float (&sv)[G][NV]) {
+  auto aggregate_store = [&](int c0, const float (&sv)[G][NV]) __attribute__((always_inline)) {
     if (out_cl) {
       float r[G];
 #pragma unroll
@@ -428,7 +428,7 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
     }
     uint32_t pre[MS][G];
     constexpr bool UNCOND = MVN_STAGE_UNCOND;
-    auto issue = [&](int c0) {
+    auto issue = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < MS; ++i)
         if (UNCOND || wfirst + kThreads * i < total) {
@@ -436,12 +436,12 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
           for (int k = 0; k < G; ++k) pre[i][k] = buf_load<TIn>(frs, goff[i], uint32_t((c0 + k) * HW * int(sizeof(TIn))));
         }
     };
-    auto commit = [&](uint4* buf) {
+    auto commit = [&](uint4* buf) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < MS; ++i)
         if (UNCOND || wfirst + kThreads * i < total) buf[t + kThreads * i] = pack<TIn>(pre[i]);
     };
-    auto consume = [&](const uint4* buf, int c0) {
+    auto consume = [&](const uint4* buf, int c0) __attribute__((always_inline)) {
       float sv[G][NV];
       sample_views(reinterpret_cast<const char*>(buf), std::true_type{}, 0, sv);
       aggregate_store(c0, sv);

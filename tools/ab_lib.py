@@ -25,18 +25,21 @@ def main():
     libs = [(os.path.basename(p), load(p)) for p in sys.argv[1:]]
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
-    for B, dt, label in ((8, torch.float32, "cfg2 f32 B=8"), (32, torch.bfloat16, "cfg3 bf16 B=32")):
-        vb = synth.volumetric_batch(B, dtype=dt, device=dev, seed=0)
+    cases = [(8, 4, torch.float32, "cfg2 f32 B=8"), (32, 4, torch.bfloat16, "cfg3 bf16 B=32")]
+    if os.environ.get("AB_CFG4"):
+        cases.append((16, 8, torch.float32, "cfg4 f32 N=8 B=16"))
+    for B, NV, dt, label in cases:
+        vb = synth.volumetric_batch(B, n_views=NV, dtype=dt, device=dev, seed=0)
         feat, proj, coords = vb.features, vb.proj, vb.coords
         E = 2 if dt == torch.bfloat16 else 4
-        nbytes = B * (E * (4 * 32 * 96 * 96 + 32 * 64 ** 3) + 12 * 64 ** 3 + 4 * 48)
+        nbytes = B * (E * (NV * 32 * 96 * 96 + 32 * 64 ** 3) + 12 * 64 ** 3 + 4 * 12 * NV)
         code = 1 if dt == torch.bfloat16 else 0
         outs = {}
         res = {}
 
         def call(lib, out, agg):
             r = lib.mvn_unproject(feat.data_ptr(), code, proj.data_ptr(), coords.data_ptr(), None, out.data_ptr(),
-                                  code, B, 4, 32, 96, 96, 64, 64, 64, agg, 0, stream)
+                                  code, B, NV, 32, 96, 96, 64, 64, 64, agg, 0, stream)
             assert r == 0, r
 
         for rnd in range(3):

@@ -90,14 +90,29 @@ def dtype_name(dt):
     return {torch.float32: "f32", torch.bfloat16: "bf16"}[dt]
 
 
+def unproject_bytes_cuboid(c, E):
+    """Algorithmic bytes of one frame's unprojection with in-kernel coordinates: features
+    read once, volume written once, cuboid (18 f32) and projections read."""
+    V3 = c["volume"] ** 3
+    return E * (c["views"] * c["channels"] * c["heatmap"] ** 2 + c["channels"] * V3) + 4 * 18 + 4 * 12 * c["views"]
+
+
+def frame_bytes_cuboid(c, E):
+    V3 = c["volume"] ** 3
+    return (E * (c["views"] * c["channels"] * c["heatmap"] ** 2 + c["channels"] * V3 + 2 * c["joints"] * V3)
+            + 4 * 2 * 18 + 4 * (12 * c["views"] + 3 * c["joints"]))
+
+
 class Workload:
-    def __init__(self, cfg, rank, world, device, seed=0):
+    def __init__(self, cfg, rank, world, device, seed=0, cuboid=False):
         self.cfg, self.rank, self.world, self.device = cfg, rank, world, device
         B = cfg["frames"]
         vb = synth.volumetric_batch(B, n_views=cfg["views"], channels=cfg["channels"], heatmap=cfg["heatmap"],
                                     volume=cfg["volume"], dtype=cfg["dtype"], device=device, seed=seed,
                                     first_frame=rank * B)
         self.feat, self.proj, self.coords = vb.features, vb.proj, vb.coords
+        if cuboid:      # coordinates formed inside both kernels (mvn_*_cuboid), never materialised
+            self.coords = vb.cuboids(device)
         self.ev = []
 
     def step(self, timed=False):
@@ -120,9 +135,9 @@ class Workload:
         return sum(t) / len(t)
 
 
-def run_config(name, args, rank, world, device):
+def run_config(name, args, rank, world, device, cuboid=False):
     cfg = CONFIGS[name]
-    wl = Workload(cfg, rank, world, device)
+    wl = Workload(cfg, rank, world, device, cuboid=cuboid)
     for _ in range(args.warmup):
         wl.step()
     torch.cuda.synchronize()
@@ -144,12 +159,12 @@ def run_config(name, args, rank, world, device):
     E = 2 if cfg["dtype"] == torch.bfloat16 else 4
     frames_total = cfg["frames"] * world * args.steps
     unproj_ms = wl.unproject_ms()
-    launch_bytes = unproject_bytes(cfg, E) * cfg["frames"]
+    launch_bytes = (unproject_bytes_cuboid if cuboid else unproject_bytes)(cfg, E) * cfg["frames"]
     achieved = launch_bytes / (unproj_ms * 1e-3) / 1e9
     return dict(
         cfg=cfg, elapsed=elapsed, fps=frames_total / elapsed, ms_per_step=elapsed / args.steps * 1e3,
         unproject_ms=unproj_ms, launch_bytes=launch_bytes, achieved_gbps=achieved,
-        path_gbps=frame_bytes(cfg, E) * frames_total / elapsed / 1e9)
+        path_gbps=(frame_bytes_cuboid if cuboid else frame_bytes)(cfg, E) * frames_total / elapsed / 1e9)
 
 
 def run_config5(args, rank, world, device):
@@ -254,6 +269,17 @@ def main():
                          unproject_achieved_gbps=s["achieved_gbps"],
                          unproject_frac=s["achieved_gbps"] / HBM_PEAK_GBPS,
                          path_algorithmic_gbps=s["path_gbps"], path_frac=s["path_gbps"] / HBM_PEAK_GBPS)
+    in_kernel_coords = None
+    if not args.no_secondary:
+        # the same workload with the coordinate volume formed inside both kernels from the
+        # per-frame cuboids instead of read from HBM
+        k = run_config(args.config, args, rank, world, device, cuboid=True)
+        in_kernel_coords = dict(workload=k["cfg"]["label"] + ", coordinates formed in-kernel from per-frame cuboids",
+                                value=k["fps"], unit="frames/s", ms_per_step=k["ms_per_step"],
+                                unproject_ms=k["unproject_ms"], unproject_algorithmic_bytes_per_launch=k["launch_bytes"],
+                                unproject_achieved_gbps=k["achieved_gbps"],
+                                unproject_frac=k["achieved_gbps"] / HBM_PEAK_GBPS,
+                                path_algorithmic_gbps=k["path_gbps"])
     cfg5 = None
     if not args.no_secondary and args.config == "2":
         cfg5 = run_config5(args, rank, world, device)
@@ -289,6 +315,7 @@ def main():
             "path_algorithmic_gbps": r["path_gbps"],
             "cpu_baseline": base,
             "secondary": secondary,
+            "in_kernel_coords": in_kernel_coords,
             "config5": cfg5,
         }
         print(json.dumps(line), flush=True)

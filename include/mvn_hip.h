@@ -15,6 +15,9 @@
  *                           path's producer of the DLT's 2D points)
  *   mvn_coord_volumes    <- mvn/models/triangulation.py:280-341 (the per-frame coordinate-
  *                           volume loop feeding unproject and soft-argmax)
+ *   mvn_unproject_cuboid, mvn_softargmax3d_cuboid
+ *                        <- op.py:99-163 / op.py:84-96 fed by triangulation.py:280-341: the
+ *                           coordinate volume formed in-kernel from the per-frame cuboid
  *   mvn_nearest_voxel    <- mvn/models/loss.py:63-67 (VolumetricCELoss's distance volume +
  *                           argmin)
  *   mvn_v2v_front        <- mvn/models/v2v.py:7-17, 145-146 (V2VModel.front_layers[0] =
@@ -172,6 +175,33 @@ int mvn_softargmax2d(const void* heatmaps, int dtype, float multiplier, int soft
  */
 int mvn_coord_volumes(const float* position, const float* centre, const float* step, const float* rot,
                       float* out, int B, int V, int transfer_cmu, void* stream);
+
+/*
+ * Unprojection and 3D soft-argmax with the coordinate volume formed in-kernel instead of
+ * read: the caller of op.py:99 / op.py:84 in triangulation.py:280-353
+ * builds coord_volumes from a per-frame cuboid and passes it straight to both ops; these
+ * entry points take the cuboid itself and never materialise the (B, V, V, V, 3) volume
+ * (12 B per voxel not read by either op).  Coordinates are bit-identical to
+ * mvn_coord_volumes on the same cuboid, so results are bit-identical to mvn_unproject_ex /
+ * mvn_softargmax3d fed that volume.
+ *   cuboids  (B, MVN_CUBOID_FLOATS) f32 per frame: position[3], centre[3], step[3], rot[9]
+ *            (the arguments of mvn_coord_volumes, interleaved per frame)
+ *   transfer_cmu  0 | 1 as in mvn_coord_volumes;  grid V x V x V
+ * mvn_unproject_cuboid needs N <= 8 (the tiled kernel); otherwise the arguments of
+ * mvn_unproject_ex / mvn_softargmax3d.
+ */
+#define MVN_CUBOID_FLOATS 18
+int mvn_unproject_cuboid(const void* feat, int feat_dtype,
+                         const float* proj, const float* cuboids, int transfer_cmu, const float* conf,
+                         void* out, int out_dtype, int out_layout,
+                         int B, int N, int C, int H, int W, int V,
+                         int agg, int align_corners, void* stream);
+int mvn_softargmax3d_cuboid(const void* vol, int vol_dtype,
+                            int64_t vol_bstride, int64_t vol_jstride,
+                            const float* cuboids, int transfer_cmu, float multiplier, int softmax,
+                            float* out_xyz, void* out_vol, int out_dtype,
+                            void* workspace, size_t workspace_bytes,
+                            int B, int J, int V, void* stream);
 
 /*
  * Nearest voxel per (frame, joint): argmin over the V^3 voxels of the f32 squared distance

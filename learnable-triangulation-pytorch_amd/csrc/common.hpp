@@ -42,6 +42,36 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// ---- cuboid coordinates (triangulation.py:280-341) ----------------------------------
+// World coordinate of grid voxel (i, j, k) of a V^3 cuboid, from the frame's geometry
+// p = position (base - side/2), cc = centre (base point), st = step, R = rotation (3x3,
+// row-major), all f32 as the host rounds them (mvn_rocm/volumetric.py).  The reference's
+// f32 op order on CPU (bit-exact against its goldens):
+//   d_k = (p_k + st_k * g_k) - cc_k          (:313-315 mul then add; :333)
+//   o_r = fma(R[r][2], d_2, fma(R[r][1], d_1, R[r][0] * d_0)) + cc_r   (rot.mm, MKL K=3; :335)
+// CMU transfer (:338-341) as an index map: out[i][j][k] = grid[i][k][V-1-j].
+// Every kernel that needs voxel coordinates either reads them from a coordinate volume
+// built by this function (mvn_coord_volumes) or calls it in-kernel (the *_cuboid entry
+// points), so both give the same bits.
+__device__ __forceinline__ void cuboid_coord(const float* __restrict__ p, const float* __restrict__ cc,
+                                             const float* __restrict__ st, const float* __restrict__ R, int V,
+                                             int i, int j, int k, int transfer, float (&o)[3]) {
+  int gx = i, gy = j, gz = k;
+  if (transfer) { gy = k; gz = V - 1 - j; }
+  const float d0 = (p[0] + st[0] * float(gx)) - cc[0];
+  const float d1 = (p[1] + st[1] * float(gy)) - cc[1];
+  const float d2 = (p[2] + st[2] * float(gz)) - cc[2];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+    o[r] = __builtin_fmaf(R[3 * r + 2], d2, __builtin_fmaf(R[3 * r + 1], d1, R[3 * r] * d0)) + cc[r];
+}
+// Packed per-frame cuboid descriptor of the *_cuboid entry points: MVN_CUBOID_FLOATS f32 =
+// position[3], centre[3], step[3], rot[9].
+__device__ __forceinline__ void cuboid_coord(const float* __restrict__ cub, int V, int i, int j, int k, int transfer,
+                                             float (&o)[3]) {
+  cuboid_coord(cub, cub + 3, cub + 6, cub + 9, V, i, j, k, transfer, o);
+}
+
 inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
 
 // XCD-aware block order (cdna_hip_programming.md §5.5 T1, bijective form): hardware deals

@@ -12,7 +12,8 @@
 //   d_k = c_k - centre_k                  (:333)
 //   r_r = fma(R[r][2], d_2, fma(R[r][1], d_1, R[r][0] * d_0))   (rot.mm, MKL K=3 order)
 //   out_r = r_r + centre_r                (:335)
-// with the CMU transfer (:338-341) as an index map: out[i][j][k] = v[i][k][V-1-j].
+// with the CMU transfer (:338-341) as an index map: out[i][j][k] = v[i][k][V-1-j]
+// (cuboid_coord, common.hpp — shared with the in-kernel coordinates of the *_cuboid ops).
 #include "common.hpp"
 
 namespace mvn {
@@ -26,22 +27,10 @@ __global__ __launch_bounds__(256) void coord_volumes(const float* __restrict__ p
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= nvox) return;
   const int i = o / (V * V), j = (o / V) % V, k = o % V;
-  // grid index of the voxel this output element takes its coordinate from
-  int gx = i, gy = j, gz = k;
-  if (transfer) { gy = k; gz = V - 1 - j; }
-  const float* p = pos + b * 3;
-  const float* cc = centre + b * 3;
-  const float* st = step + b * 3;
-  const float* R = rot + b * 9;
-  const float d0 = (p[0] + st[0] * float(gx)) - cc[0];
-  const float d1 = (p[1] + st[1] * float(gy)) - cc[1];
-  const float d2 = (p[2] + st[2] * float(gz)) - cc[2];
+  float c[3];
+  cuboid_coord(pos + b * 3, centre + b * 3, step + b * 3, rot + b * 9, V, i, j, k, transfer, c);
   float* op = out + (size_t(b) * nvox + o) * 3;
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    const float rr = __builtin_fmaf(R[3 * r + 2], d2, __builtin_fmaf(R[3 * r + 1], d1, R[3 * r] * d0));
-    op[r] = rr + cc[r];
-  }
+  op[0] = c[0]; op[1] = c[1]; op[2] = c[2];
 }
 
 }  // namespace

@@ -124,17 +124,35 @@ __device__ __forceinline__ float wave_sum63(float v) {
 template <typename T, bool SOFTMAX>
 __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     const T* __restrict__ vol, long long bstride, long long jstride, const float* __restrict__ coords,
-    float mult, float* __restrict__ part, int J, int nvox, int nchunk, bool vec_ok) {
+    const float* __restrict__ cub, int V, int transfer, float mult, float* __restrict__ part, int J, int nvox,
+    int nchunk, bool vec_ok) {
   constexpr int VEC = Vec<T>::n;
   constexpr int RUNS = kPartChunk / (kWave * VEC);
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const int chunk = blockIdx.x * (kSaBlock / kWave) + wid, b = blockIdx.y;
   if (chunk >= nchunk) return;                         // whole wave; this kernel has no barriers
   const T* vb = vol + b * bstride;
-  const float* cb = coords + size_t(b) * nvox * 3;
+  const float* cb = cub ? nullptr : coords + size_t(b) * nvox * 3;
   const float fill = SOFTMAX ? -INFINITY : 0.f;
 
   float c[RUNS][3 * VEC];
+  if (cub) {
+    // coordinates formed in-kernel from the frame's cuboid (bit-identical to mvn_coord_volumes)
+    const float* cf = cub + size_t(b) * MVN_CUBOID_FLOATS;
+#pragma unroll
+    for (int r = 0; r < RUNS; ++r) {
+      const int i = chunk * kPartChunk + r * kWave * VEC + lane * VEC;
+      int gi = i / (V * V), gj = (i / V) % V, gk = i % V;
+#pragma unroll
+      for (int u = 0; u < VEC; ++u) {
+        float o[3];
+        cuboid_coord(cf, V, gi, gj, gk, transfer, o);
+        const bool in = i + u < nvox;
+        c[r][3 * u] = in ? o[0] : 0.f; c[r][3 * u + 1] = in ? o[1] : 0.f; c[r][3 * u + 2] = in ? o[2] : 0.f;
+        if (++gk == V) { gk = 0; if (++gj == V) { gj = 0; ++gi; } }
+      }
+    }
+  } else {
 #pragma unroll
   for (int r = 0; r < RUNS; ++r) {
     const int i = chunk * kPartChunk + r * kWave * VEC + lane * VEC;
@@ -149,6 +167,7 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
 #pragma unroll
       for (int u = 0; u < 3 * VEC; ++u) c[r][u] = (i + u / 3 < nvox) ? cb[size_t(i) * 3 + u] : 0.f;
     }
+  }
   }
   auto load = [&](int j, float (&x)[RUNS][VEC]) {
 #pragma unroll
@@ -276,15 +295,15 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_finalize(
 }
 
 template <typename T, typename TO, bool SOFTMAX>
-int launch(const void* vol, long long bs, long long js, const float* coords, float mult, float* xyz,
-           void* out, float* part, int B, int J, int nvox, hipStream_t st) {
+int launch(const void* vol, long long bs, long long js, const float* coords, const float* cub, int V, int transfer,
+           float mult, float* xyz, void* out, float* part, int B, int J, int nvox, hipStream_t st) {
   const int nchunk = (nvox + kSaChunk - 1) / kSaChunk;       // pass-2 blocks per (b, j)
   const int npart = (nvox + kPartChunk - 1) / kPartChunk;     // pass-1 partials per (b, j)
   const bool vec_ok = (reinterpret_cast<uintptr_t>(vol) % 16 == 0) && (bs * sizeof(T)) % 16 == 0 &&
                       (js * sizeof(T)) % 16 == 0 && (nvox % 8 == 0) &&
                       (out == nullptr || reinterpret_cast<uintptr_t>(out) % 16 == 0);
   softargmax_partials<T, SOFTMAX><<<dim3((npart + kSaBlock / kWave - 1) / (kSaBlock / kWave), B), kSaBlock, 0, st>>>(
-      static_cast<const T*>(vol), bs, js, coords, mult, part, J, nvox, npart, vec_ok);
+      static_cast<const T*>(vol), bs, js, coords, cub, V, transfer, mult, part, J, nvox, npart, vec_ok);
   if (!launch_ok()) return MVN_ERR_LAUNCH;
   float* stat = part + size_t(B) * J * npart * kPartial;
   softargmax_combine<SOFTMAX><<<(B * J + kSaBlock / kWave - 1) / (kSaBlock / kWave), kSaBlock, 0, st>>>(
@@ -297,11 +316,17 @@ int launch(const void* vol, long long bs, long long js, const float* coords, flo
 }
 
 template <typename T, typename TO>
-int launch_mode(int softmax, const void* vol, long long bs, long long js, const float* coords, float mult,
-                float* xyz, void* out, float* part, int B, int J, int nvox, hipStream_t st) {
-  return softmax ? launch<T, TO, true>(vol, bs, js, coords, mult, xyz, out, part, B, J, nvox, st)
-                 : launch<T, TO, false>(vol, bs, js, coords, mult, xyz, out, part, B, J, nvox, st);
+int launch_mode(int softmax, const void* vol, long long bs, long long js, const float* coords, const float* cub,
+                int V, int transfer, float mult, float* xyz, void* out, float* part, int B, int J, int nvox,
+                hipStream_t st) {
+  return softmax ? launch<T, TO, true>(vol, bs, js, coords, cub, V, transfer, mult, xyz, out, part, B, J, nvox, st)
+                 : launch<T, TO, false>(vol, bs, js, coords, cub, V, transfer, mult, xyz, out, part, B, J, nvox, st);
 }
+
+int softargmax_entry(const void* vol, int vol_dtype, int64_t vol_bstride, int64_t vol_jstride, const float* coords,
+                     const float* cub, int transfer, float multiplier, int softmax, float* out_xyz, void* out_vol,
+                     int out_dtype, void* workspace, size_t workspace_bytes, int B, int J, int Vx, int Vy, int Vz,
+                     void* stream);
 
 }  // namespace
 }  // namespace mvn
@@ -313,13 +338,15 @@ extern "C" size_t mvn_softargmax3d_workspace_bytes(int B, int J, int Vx, int Vy,
   return size_t(B) * J * (npart * mvn::kPartial + 2) * sizeof(float);   // partials + (max, 1/sum)
 }
 
-extern "C" int mvn_softargmax3d(const void* vol, int vol_dtype, int64_t vol_bstride, int64_t vol_jstride,
-                                const float* coords, float multiplier, int softmax, float* out_xyz,
-                                void* out_vol, int out_dtype, void* workspace, size_t workspace_bytes,
-                                int B, int J, int Vx, int Vy, int Vz, void* stream) {
-  using namespace mvn;
-  if (!vol || !coords || !out_xyz) return MVN_ERR_ARG;
+namespace mvn {
+namespace {
+int softargmax_entry(const void* vol, int vol_dtype, int64_t vol_bstride, int64_t vol_jstride, const float* coords,
+                     const float* cub, int transfer, float multiplier, int softmax, float* out_xyz, void* out_vol,
+                     int out_dtype, void* workspace, size_t workspace_bytes, int B, int J, int Vx, int Vy, int Vz,
+                     void* stream) {
+  if (!vol || !(coords || cub) || !out_xyz) return MVN_ERR_ARG;
   if (softmax != 0 && softmax != 1) return MVN_ERR_ARG;
+  if (transfer != 0 && transfer != 1) return MVN_ERR_ARG;
   if (B <= 0 || J <= 0 || Vx <= 0 || Vy <= 0 || Vz <= 0 || B > 65535 || J > 65535) return MVN_ERR_SHAPE;
   const long long nvox = (long long)Vx * Vy * Vz;
   if (nvox > (1LL << 30)) return MVN_ERR_SHAPE;
@@ -330,10 +357,31 @@ extern "C" int mvn_softargmax3d(const void* vol, int vol_dtype, int64_t vol_bstr
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int n = int(nvox);
   if (vol_dtype == MVN_DTYPE_F32 && out_dtype == MVN_DTYPE_F32)
-    return launch_mode<float, float>(softmax, vol, vol_bstride, vol_jstride, coords, multiplier, out_xyz, out_vol, part, B, J, n, st);
+    return launch_mode<float, float>(softmax, vol, vol_bstride, vol_jstride, coords, cub, Vx, transfer, multiplier, out_xyz, out_vol, part, B, J, n, st);
   if (vol_dtype == MVN_DTYPE_BF16 && out_dtype == MVN_DTYPE_BF16)
-    return launch_mode<uint16_t, uint16_t>(softmax, vol, vol_bstride, vol_jstride, coords, multiplier, out_xyz, out_vol, part, B, J, n, st);
+    return launch_mode<uint16_t, uint16_t>(softmax, vol, vol_bstride, vol_jstride, coords, cub, Vx, transfer, multiplier, out_xyz, out_vol, part, B, J, n, st);
   if (vol_dtype == MVN_DTYPE_BF16 && out_dtype == MVN_DTYPE_F32)
-    return launch_mode<uint16_t, float>(softmax, vol, vol_bstride, vol_jstride, coords, multiplier, out_xyz, out_vol, part, B, J, n, st);
+    return launch_mode<uint16_t, float>(softmax, vol, vol_bstride, vol_jstride, coords, cub, Vx, transfer, multiplier, out_xyz, out_vol, part, B, J, n, st);
   return MVN_ERR_DTYPE;
+}
+}  // namespace
+}  // namespace mvn
+
+extern "C" int mvn_softargmax3d(const void* vol, int vol_dtype, int64_t vol_bstride, int64_t vol_jstride,
+                                const float* coords, float multiplier, int softmax, float* out_xyz,
+                                void* out_vol, int out_dtype, void* workspace, size_t workspace_bytes,
+                                int B, int J, int Vx, int Vy, int Vz, void* stream) {
+  if (!coords) return MVN_ERR_ARG;
+  return mvn::softargmax_entry(vol, vol_dtype, vol_bstride, vol_jstride, coords, nullptr, 0, multiplier, softmax,
+                               out_xyz, out_vol, out_dtype, workspace, workspace_bytes, B, J, Vx, Vy, Vz, stream);
+}
+
+extern "C" int mvn_softargmax3d_cuboid(const void* vol, int vol_dtype, int64_t vol_bstride, int64_t vol_jstride,
+                                       const float* cuboids, int transfer_cmu, float multiplier, int softmax,
+                                       float* out_xyz, void* out_vol, int out_dtype, void* workspace,
+                                       size_t workspace_bytes, int B, int J, int V, void* stream) {
+  if (!cuboids) return MVN_ERR_ARG;
+  return mvn::softargmax_entry(vol, vol_dtype, vol_bstride, vol_jstride, nullptr, cuboids, transfer_cmu, multiplier,
+                               softmax, out_xyz, out_vol, out_dtype, workspace, workspace_bytes, B, J, V, V, V,
+                               stream);
 }

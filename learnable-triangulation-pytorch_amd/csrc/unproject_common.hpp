@@ -180,8 +180,11 @@ __device__ __forceinline__ float aggregate(const float (&s)[NV], int N, const fl
 
 // Launchers (defined in unproject_tiled.hip); return MVN_OK or an error code.
 template <int AGG, typename TIn, typename TOut>
-int launch_tiled(const void* feat, const float* P, const float* coords, const float* conf, void* out, int B,
-                 int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, int out_cl, hipStream_t s);
+// cub != nullptr: voxel coordinates formed in-kernel from the per-frame cuboids (coords unused;
+// Vx = Vy = Vz), see cuboid_coord in common.hpp.
+int launch_tiled(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
+                 const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+                 int align_corners, int out_cl, hipStream_t s);
 
 }  // namespace unproj
 }  // namespace mvn

@@ -195,8 +195,8 @@ template <int AGG, typename TIn, typename TOut, int NV, bool EXACT>
 __global__ __launch_bounds__(TileShape<NV>::THREADS)
 __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
-    const float* __restrict__ conf, TOut* __restrict__ out, int B, int n_views, int C, int H, int W, int Vx,
-    int Vy, int Vz, int align_corners, int budget, int out_cl) {
+    const float* __restrict__ cub, int transfer, const float* __restrict__ conf, TOut* __restrict__ out, int B,
+    int n_views, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, int budget, int out_cl) {
   const int N = EXACT ? NV : n_views;
   using S = TileShape<NV>;
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ, kThreads = S::THREADS, kBuf = S::SLOTS;
@@ -246,8 +246,15 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
   const int X = tx * TX + t / (TZ * TY), Y = ty * TY + (t / TZ) % TY, Z = tz * TZ + t % TZ;
   const bool act = (X < Vx) & (Y < Vy) & (Z < Vz);
   const int vox = act ? (X * Vy + Y) * Vz + Z : 0;
-  const float* cp = coords + (size_t(b) * nvox + vox) * 3;
-  const float cx = cp[0], cy = cp[1], cz = cp[2];
+  float cx, cy, cz;
+  if (cub) {                          // block-uniform: formed in-kernel, bit-identical to the volume
+    float o[3];
+    cuboid_coord(cub + b * MVN_CUBOID_FLOATS, Vx, X, Y, Z, transfer, o);
+    cx = o[0]; cy = o[1]; cz = o[2];
+  } else {
+    const float* cp = coords + (size_t(b) * nvox + vox) * 3;
+    cx = cp[0]; cy = cp[1]; cz = cp[2];
+  }
 
   // ---- per-view geometry: footprint base pixel, weights, "samples the image" flag --
   int fx[NV], fy[NV];
@@ -498,8 +505,9 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
 }  // namespace
 
 template <int AGG, typename TIn, typename TOut>
-int launch_tiled(const void* feat, const float* P, const float* coords, const float* conf, void* out, int B,
-                 int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, int out_cl, hipStream_t s) {
+int launch_tiled(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
+                 const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+                 int align_corners, int out_cl, hipStream_t s) {
   if (out_cl && C % 4 != 0) return MVN_ERR_SHAPE;
   // 32-bit buffer offsets: a frame's maps and volume must stay below 2 GiB
   if ((long long)N * C * H * W * sizeof(TIn) >= (1LL << 31) ||
@@ -516,8 +524,8 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
                          ((Vz + S::TZ - 1) / S::TZ);
     if (nb > INT_MAX) return false;
     unproject_tiled<AGG, TIn, TOut, NV, decltype(exact)::value><<<int(nb), S::THREADS, 0, s>>>(
-        static_cast<const TIn*>(feat), P, coords, conf, static_cast<TOut*>(out), B, N, C, H, W, Vx, Vy, Vz,
-        align_corners, budget, out_cl);
+        static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, N, C, H, W,
+        Vx, Vy, Vz, align_corners, budget, out_cl);
     return true;
   };
   using I4 = std::integral_constant<int, 4>;
@@ -530,12 +538,12 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
 }
 
 #define MVN_INSTANTIATE(AGG)                                                                                   \
-  template int launch_tiled<AGG, float, float>(const void*, const float*, const float*, const float*, void*,    \
+  template int launch_tiled<AGG, float, float>(const void*, const float*, const float*, const float*, int, const float*, void*,    \
                                                int, int, int, int, int, int, int, int, int, int, hipStream_t);       \
-  template int launch_tiled<AGG, uint16_t, uint16_t>(const void*, const float*, const float*, const float*,     \
+  template int launch_tiled<AGG, uint16_t, uint16_t>(const void*, const float*, const float*, const float*, int, const float*,     \
                                                      void*, int, int, int, int, int, int, int, int, int, int,   \
                                                      hipStream_t);                                              \
-  template int launch_tiled<AGG, uint16_t, float>(const void*, const float*, const float*, const float*, void*, \
+  template int launch_tiled<AGG, uint16_t, float>(const void*, const float*, const float*, const float*, int, const float*, void*, \
                                                   int, int, int, int, int, int, int, int, int, int, hipStream_t);
 MVN_INSTANTIATE(MVN_AGG_SUM)
 MVN_INSTANTIATE(MVN_AGG_MAX)

@@ -35,6 +35,11 @@ SIGNATURES = {
     "mvn_softargmax2d": (_c_int, [_c_void_p, _c_int, _c_float, _c_int, _c_void_p, _c_void_p, _c_int]
                          + [_c_int] * 4 + [_c_void_p]),
     "mvn_coord_volumes": (_c_int, [_c_void_p] * 5 + [_c_int, _c_int, _c_int, _c_void_p]),
+    "mvn_unproject_cuboid": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
+                                      _c_int, _c_int] + [_c_int] * 6 + [_c_int, _c_int, _c_void_p]),
+    "mvn_softargmax3d_cuboid": (_c_int, [_c_void_p, _c_int, _c_i64, _c_i64, _c_void_p, _c_int, _c_float, _c_int,
+                                         _c_void_p, _c_void_p, _c_int, _c_void_p, _c_size_t]
+                                + [_c_int] * 3 + [_c_void_p]),
     "mvn_nearest_voxel": (_c_int, [_c_void_p] * 3 + [_c_int] * 5 + [_c_void_p]),
     "mvn_unproject_ex": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int]
                          + [_c_int] * 8 + [_c_int, _c_int, _c_void_p]),

@@ -97,6 +97,58 @@ def _(vol, coords, softmax, multiplier, return_volume, out_dtype):
     return xyz, vol.new_empty(shape, dtype=_CODE_DTYPE[out_dtype])
 
 
+# --------------------------------------------------------------------------- in-kernel coordinates
+@torch.library.custom_op("mvn_rocm::unproject_cuboid", mutates_args=())
+def unproject_cuboid(feat: Tensor, proj: Tensor, cuboids: Tensor, volume_size: int, transfer: bool,
+                     conf: Optional[Tensor], agg: int, align_corners: bool, out_dtype: int) -> Tensor:
+    """unproject with coordinates formed in-kernel from cuboids (B, 18) f32 (V^3 grid)."""
+    _require_gpu(feat, proj, cuboids, conf)
+    B, N, C, H, W = feat.shape
+    V = int(volume_size)
+    out = torch.empty((B, C, V, V, V), dtype=_CODE_DTYPE[out_dtype], device=feat.device)
+    code = _lib.load().mvn_unproject_cuboid(
+        feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), cuboids.data_ptr(), int(transfer), _ptr(conf),
+        out.data_ptr(), out_dtype, _lib.MVN_LAYOUT_NCDHW, B, N, C, H, W, V, agg, int(align_corners), _stream(feat))
+    _lib.check(code, "mvn_unproject_cuboid")
+    return out
+
+
+@unproject_cuboid.register_fake
+def _(feat, proj, cuboids, volume_size, transfer, conf, agg, align_corners, out_dtype):
+    B, N, C = feat.shape[:3]
+    V = int(volume_size)
+    return feat.new_empty((B, C, V, V, V), dtype=_CODE_DTYPE[out_dtype])
+
+
+@torch.library.custom_op("mvn_rocm::softargmax3d_cuboid", mutates_args=())
+def softargmax3d_cuboid(vol: Tensor, cuboids: Tensor, transfer: bool, softmax: bool, multiplier: float,
+                        return_volume: bool, out_dtype: int) -> Tuple[Tensor, Tensor]:
+    """softargmax3d with coordinates formed in-kernel from cuboids (B, 18) f32."""
+    _require_gpu(vol, cuboids)
+    B, J, V = vol.shape[:3]
+    xyz = torch.empty((B, J, 3), dtype=torch.float32, device=vol.device)
+    if return_volume:
+        out = torch.empty(tuple(vol.shape), dtype=_CODE_DTYPE[out_dtype], device=vol.device)
+    else:
+        out = torch.empty((0,), dtype=_CODE_DTYPE[out_dtype], device=vol.device)
+    lib = _lib.load()
+    ws_bytes = lib.mvn_softargmax3d_workspace_bytes(B, J, V, V, V)
+    ws = torch.empty((ws_bytes + 15) // 16 * 4, dtype=torch.float32, device=vol.device)
+    code = lib.mvn_softargmax3d_cuboid(
+        vol.data_ptr(), _DTYPE_CODE[vol.dtype], vol.stride(0), vol.stride(1), cuboids.data_ptr(), int(transfer),
+        float(multiplier), int(softmax), xyz.data_ptr(), out.data_ptr() if return_volume else None,
+        out_dtype, ws.data_ptr(), ws.numel() * 4, B, J, V, _stream(vol))
+    _lib.check(code, "mvn_softargmax3d_cuboid")
+    return xyz, out
+
+
+@softargmax3d_cuboid.register_fake
+def _(vol, cuboids, transfer, softmax, multiplier, return_volume, out_dtype):
+    B, J = vol.shape[:2]
+    shape = tuple(vol.shape) if return_volume else (0,)
+    return vol.new_empty((B, J, 3), dtype=torch.float32), vol.new_empty(shape, dtype=_CODE_DTYPE[out_dtype])
+
+
 # --------------------------------------------------------------------------- 2D soft-argmax
 @torch.library.custom_op("mvn_rocm::softargmax2d", mutates_args=())
 def softargmax2d(hm: Tensor, softmax: bool, multiplier: float, return_maps: bool,

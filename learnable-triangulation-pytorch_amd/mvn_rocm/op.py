@@ -23,6 +23,11 @@ def aggregation_code(method: str) -> int:
     raise ValueError("Unknown volume_aggregation_method: {}".format(method))   # op.py:161
 
 
+def _is_cuboids(x) -> bool:
+    from .volumetric import Cuboids
+    return isinstance(x, Cuboids)
+
+
 def _dtype_code(dtype: torch.dtype) -> int:
     if dtype == torch.float32:
         return _lib.MVN_DTYPE_F32
@@ -43,21 +48,31 @@ def unproject_heatmaps(heatmaps, proj_matricies, coord_volumes, volume_aggregati
     heatmap dtype (float32 for float32 input, as in the reference).
     """
     agg = aggregation_code(volume_aggregation_method)
+    cub = coord_volumes if _is_cuboids(coord_volumes) else None
     if agg == _lib.MVN_AGG_CONF and vol_confidences is None:
         raise TypeError("volume_aggregation_method '{}' needs vol_confidences".format(volume_aggregation_method))
     feat = heatmaps.contiguous()
     if feat.dtype not in (torch.float32, torch.bfloat16):
         feat = feat.float()
     proj = proj_matricies.float().contiguous()
-    coords = coord_volumes.float().contiguous()
     conf = vol_confidences.float().contiguous() if agg == _lib.MVN_AGG_CONF else None
     if proj.shape[:2] != feat.shape[:2] or proj.shape[2:] != (3, 4):
         raise RuntimeError(f"proj_matricies shape {tuple(proj.shape)} does not match heatmaps {tuple(feat.shape)}")
-    if coords.dim() != 5 or coords.shape[0] != feat.shape[0] or coords.shape[4] != 3:
-        raise RuntimeError(f"coord_volumes must be (B, Vx, Vy, Vz, 3), got {tuple(coords.shape)}")
     if conf is not None and conf.shape != feat.shape[:3]:
         raise RuntimeError(f"vol_confidences must be {tuple(feat.shape[:3])}, got {tuple(conf.shape)}")
     od = _dtype_code(out_dtype if out_dtype is not None else feat.dtype)
+    if cub is not None:
+        if cub.batch != feat.shape[0]:
+            raise RuntimeError(f"cuboids for {cub.batch} frames, heatmaps have {feat.shape[0]}")
+        if feat.shape[1] > 8:
+            # in-kernel coordinates need the tiled kernel (N <= 8): materialise the volume
+            coord_volumes, cub = cub.coord_volumes(), None
+        else:
+            return UnprojectCuboidFunction.apply(feat, proj, cub.params, cub.volume_size, cub.transfer, conf, agg,
+                                                 bool(align_corners), od)
+    coords = coord_volumes.float().contiguous()
+    if coords.dim() != 5 or coords.shape[0] != feat.shape[0] or coords.shape[4] != 3:
+        raise RuntimeError(f"coord_volumes must be (B, Vx, Vy, Vz, 3), got {tuple(coords.shape)}")
     return UnprojectFunction.apply(feat, proj, coords, conf, agg, bool(align_corners), od)
 
 
@@ -77,10 +92,17 @@ def integrate_tensor_3d_with_coordinates(volumes, coord_volumes, softmax=True, *
     Vx, Vy, Vz = vol.shape[2:]
     if vol.stride(4) != 1 or vol.stride(3) != Vz or vol.stride(2) != Vy * Vz:
         vol = vol.contiguous()
+    od = _dtype_code(out_dtype if out_dtype is not None else vol.dtype)
+    if _is_cuboids(coord_volumes):
+        cub = coord_volumes
+        if cub.shape != (vol.shape[0], Vx, Vy, Vz, 3):
+            raise RuntimeError(f"cuboids {tuple(cub.shape)} do not match volumes {tuple(vol.shape)}")
+        xyz, out = SoftArgmaxCuboidFunction.apply(vol, cub.params, cub.volume_size, cub.transfer, bool(softmax),
+                                                  float(multiplier), bool(return_volumes), od)
+        return xyz, (out if return_volumes else None)
     coords = coord_volumes.float().contiguous()
     if coords.shape != (vol.shape[0], Vx, Vy, Vz, 3):
         raise RuntimeError(f"coord_volumes {tuple(coords.shape)} does not match volumes {tuple(vol.shape)}")
-    od = _dtype_code(out_dtype if out_dtype is not None else vol.dtype)
     xyz, out = SoftArgmaxFunction.apply(vol, coords, bool(softmax), float(multiplier), bool(return_volumes), od)
     return xyz, (out if return_volumes else None)
 
@@ -135,6 +157,57 @@ class SoftArgmaxFunction(torch.autograd.Function):
     def backward(ctx, grad_xyz, grad_out):
         from . import _backward
         return _backward.softargmax_backward(ctx, grad_xyz, grad_out)
+
+
+class UnprojectCuboidFunction(torch.autograd.Function):
+    """UnprojectFunction with the coordinates formed in-kernel from per-frame cuboids
+    (csrc/unproject_tiled.hip, cuboid_coord); backward materialises the coordinate volume
+    (one small kernel) and runs the same backward kernel."""
+
+    @staticmethod
+    def forward(ctx, feat, proj, cub, V, transfer, conf, agg, align_corners, out_dtype):
+        out = _ops.unproject_cuboid(feat, proj, cub, V, transfer, conf, agg, align_corners, out_dtype)
+        ctx.save_for_backward(feat, proj, cub, conf)
+        ctx.cfg = (V, transfer, agg, align_corners)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        from . import _backward
+        from .volumetric import Cuboids
+        feat, proj, cub, conf = ctx.saved_tensors
+        V, transfer, agg, align_corners = ctx.cfg
+        want_conf = conf is not None and ctx.needs_input_grad[5]
+        if not (ctx.needs_input_grad[0] or want_conf):
+            return (None,) * 9
+        coords = Cuboids(cub, V, transfer).coord_volumes()
+        gfeat, gconf = _backward.unproject_bwd(feat, proj, coords, conf, grad_out, agg, align_corners, want_conf)
+        return (gfeat if ctx.needs_input_grad[0] else None, None, None, None, None,
+                gconf if want_conf else None, None, None, None)
+
+
+class SoftArgmaxCuboidFunction(torch.autograd.Function):
+    """SoftArgmaxFunction with in-kernel coordinates (csrc/softargmax.hip, cuboid_coord)."""
+
+    @staticmethod
+    def forward(ctx, vol, cub, V, transfer, softmax, multiplier, return_volume, out_dtype):
+        xyz, out = _ops.softargmax3d_cuboid(vol, cub, transfer, softmax, multiplier, return_volume, out_dtype)
+        ctx.save_for_backward(vol, cub)
+        ctx.cfg = (V, transfer, softmax, multiplier, return_volume)
+        return xyz, out
+
+    @staticmethod
+    def backward(ctx, grad_xyz, grad_out):
+        from . import _backward
+        from .volumetric import Cuboids
+        vol, cub = ctx.saved_tensors
+        V, transfer, softmax, multiplier, return_volume = ctx.cfg
+        if not ctx.needs_input_grad[0]:
+            return (None,) * 8
+        coords = Cuboids(cub, V, transfer).coord_volumes()
+        gv = grad_out if (return_volume and grad_out is not None and grad_out.numel() > 0) else None
+        gin = _backward.softargmax3d_bwd(vol, coords, softmax, multiplier, grad_xyz, gv)
+        return (gin,) + (None,) * 7
 
 
 class SoftArgmax2dFunction(torch.autograd.Function):

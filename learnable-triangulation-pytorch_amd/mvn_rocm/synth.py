@@ -124,13 +124,23 @@ class VolumetricBatch:
     proj: torch.Tensor            # (B, N, 3, 4) float32, heatmap resolution
     coords: torch.Tensor          # (B, V, V, V, 3) float32
     base_points: torch.Tensor     # (B, 3)
+    base_points64: np.ndarray = None   # (B, 3) float64 (what the coordinate volumes are built from)
+    thetas: np.ndarray = None          # (B,) rotation angles
+    kind: str = "coco"
+
+    def cuboids(self, device="cuda"):
+        """The same coordinate volumes as per-frame cuboids (in-kernel coordinates,
+        mvn_rocm.volumetric.Cuboids)."""
+        from .volumetric import build_cuboids
+        return build_cuboids(self.base_points64, CUBOID_SIDE, self.coords.shape[1], self.thetas, self.kind,
+                             device=device)
 
 
 def volumetric_batch(batch: int, n_views: int = 4, channels: int = 32, heatmap: int = HEATMAP_SIZE,
                      volume: int = VOLUME_SIZE, dtype=torch.float32, device="cpu", seed: int = 0,
                      first_frame: int = 0, rotate: bool = True, kind: str = "coco") -> VolumetricBatch:
     """Frames [first_frame, first_frame + batch) of the seeded synthetic workload."""
-    feats, projs, coords, bases = [], [], [], []
+    feats, projs, coords, bases, bases64, thetas = [], [], [], [], [], []
     for f in range(first_frame, first_frame + batch):
         rng = _frame_rng(seed + 1, f)
         cams = ring_cameras(n_views, rng)
@@ -138,6 +148,8 @@ def volumetric_batch(batch: int, n_views: int = 4, channels: int = 32, heatmap: 
         base = np.array([rng.uniform(-500, 500), rng.uniform(-500, 500), rng.uniform(800, 1000)])
         theta = rng.uniform(0.0, 2.0 * math.pi) if rotate else 0.0
         bases.append(torch.from_numpy(base).to(torch.float32))
+        bases64.append(base)
+        thetas.append(theta)
         coords.append(coord_volume(base, theta, volume, kind=kind, device=device))
         g = torch.Generator(device=device)
         g.manual_seed(seed * 1_000_003 + f)
@@ -146,7 +158,8 @@ def volumetric_batch(batch: int, n_views: int = 4, channels: int = 32, heatmap: 
         features=torch.stack(feats).to(dtype),
         proj=torch.stack(projs).to(device),
         coords=torch.stack(coords),
-        base_points=torch.stack(bases).to(device))
+        base_points=torch.stack(bases).to(device),
+        base_points64=np.stack(bases64), thetas=np.asarray(thetas, dtype=np.float64), kind=kind)
 
 
 def blob_volumes(coords: torch.Tensor, n_joints: int = 17, seed: int = 0, first_frame: int = 0,

@@ -31,14 +31,57 @@ def rotation_matrix(axis, theta: float) -> np.ndarray:
                      [2 * (bd + ac), 2 * (cd - ab), aa + dd - bb - cc]])
 
 
-def build_coord_volumes(base_points, cuboid_side: float, volume_size: int, theta=0.0, kind: str = "coco",
-                        transfer_cmu_to_human36m: bool = False, device="cuda"):
-    """(B, V, V, V, 3) float32 coordinate volumes on ``device``.
+CUBOID_FLOATS = 18     # MVN_CUBOID_FLOATS: position[3], centre[3], step[3], rot[9] per frame
 
-    base_points: (B, 3) float64 array (the pelvis of each frame, triangulation.py:288-293);
-    theta: scalar or (B,) rotation angles (0 in eval, uniform [0, 2pi) in training,
-    triangulation.py:320-323); kind: 'coco' rotates about y, 'mpii' about z (:325-328).
+
+class Cuboids:
+    """Per-frame cuboid geometry of the volumetric model (triangulation.py:280-341), on the GPU.
+
+    ``params`` (B, 18) f32 = position, centre, step, rotation per frame, rounded to f32 as
+    the reference's torch code rounds them.  ``coord_volumes()`` materialises the
+    (B, V, V, V, 3) volume (``mvn_coord_volumes``); ``op.unproject_heatmaps`` and
+    ``op.integrate_tensor_3d_with_coordinates`` also accept a ``Cuboids`` in place of the
+    volume and then form the coordinates in-kernel (``mvn_*_cuboid``), bit-identically.
     """
+
+    def __init__(self, params: torch.Tensor, volume_size: int, transfer_cmu_to_human36m: bool = False):
+        if params.dim() != 2 or params.shape[1] != CUBOID_FLOATS or params.dtype != torch.float32:
+            raise RuntimeError(f"cuboid params must be (B, {CUBOID_FLOATS}) float32, got {tuple(params.shape)}")
+        self.params = params.contiguous()
+        self.volume_size = int(volume_size)
+        self.transfer = bool(transfer_cmu_to_human36m)
+
+    @property
+    def batch(self) -> int:
+        return self.params.shape[0]
+
+    @property
+    def shape(self):
+        """Shape of the coordinate volume these cuboids stand for."""
+        V = self.volume_size
+        return torch.Size((self.batch, V, V, V, 3))
+
+    @property
+    def device(self):
+        return self.params.device
+
+    def coord_volumes(self) -> torch.Tensor:
+        """(B, V, V, V, 3) f32 coordinate volume (one kernel launch)."""
+        _require_gpu(self.params)
+        B, V = self.batch, self.volume_size
+        out = torch.empty((B, V, V, V, 3), dtype=torch.float32, device=self.device)
+        # mvn_coord_volumes takes the four fields as separate (B, k) arrays
+        fields = [self.params[:, 0:3].contiguous(), self.params[:, 3:6].contiguous(),
+                  self.params[:, 6:9].contiguous(), self.params[:, 9:18].contiguous()]
+        code = _lib.load().mvn_coord_volumes(*(f.data_ptr() for f in fields), out.data_ptr(), B, V,
+                                             int(self.transfer), torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(code, "mvn_coord_volumes")
+        return out
+
+
+def build_cuboids(base_points, cuboid_side: float, volume_size: int, theta=0.0, kind: str = "coco",
+                  transfer_cmu_to_human36m: bool = False, device="cuda") -> Cuboids:
+    """Per-frame cuboids of triangulation.py:280-341 (same arguments as build_coord_volumes)."""
     base = np.asarray(base_points.detach().cpu().numpy() if torch.is_tensor(base_points) else base_points,
                       dtype=np.float64).reshape(-1, 3)
     B, V = base.shape[0], int(volume_size)
@@ -54,14 +97,18 @@ def build_coord_volumes(base_points, cuboid_side: float, volume_size: int, theta
     step = np.broadcast_to((sides / (V - 1)).astype(np.float32), (B, 3)).copy()     # :313-315
     centre = base.astype(np.float32)                                                 # :330
     rot = np.stack([rotation_matrix(axis, t) for t in thetas]).astype(np.float32)    # volumetric.py:106
-    dev = torch.device(device)
-    host = torch.from_numpy(np.concatenate([position.ravel(), centre.ravel(), step.ravel(), rot.ravel()]))
-    params = host.to(dev)
-    _require_gpu(params)
-    out = torch.empty((B, V, V, V, 3), dtype=torch.float32, device=dev)
-    p = params.data_ptr()
-    code = _lib.load().mvn_coord_volumes(p, p + 12 * B, p + 24 * B, p + 36 * B, out.data_ptr(), B, V,
-                                         int(bool(transfer_cmu_to_human36m)),
-                                         torch.cuda.current_stream(dev).cuda_stream)
-    _lib.check(code, "mvn_coord_volumes")
-    return out
+    host = np.concatenate([position, centre, step, rot.reshape(B, 9)], axis=1)
+    params = torch.from_numpy(np.ascontiguousarray(host)).to(torch.device(device))
+    return Cuboids(params, V, transfer_cmu_to_human36m)
+
+
+def build_coord_volumes(base_points, cuboid_side: float, volume_size: int, theta=0.0, kind: str = "coco",
+                        transfer_cmu_to_human36m: bool = False, device="cuda"):
+    """(B, V, V, V, 3) float32 coordinate volumes on ``device``.
+
+    base_points: (B, 3) float64 array (the pelvis of each frame, triangulation.py:288-293);
+    theta: scalar or (B,) rotation angles (0 in eval, uniform [0, 2pi) in training,
+    triangulation.py:320-323); kind: 'coco' rotates about y, 'mpii' about z (:325-328).
+    """
+    return build_cuboids(base_points, cuboid_side, volume_size, theta, kind, transfer_cmu_to_human36m,
+                         device).coord_volumes()

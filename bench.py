@@ -250,6 +250,8 @@ def main():
     ap.add_argument("--config", default="2", choices=[k for k in sorted(CONFIGS) if k != "5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-in-kernel-coords", action="store_true",
+                    help="skip the in-kernel-coordinates run (keeps rocprof kernel means per variant clean)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -270,7 +272,7 @@ def main():
                          unproject_frac=s["achieved_gbps"] / HBM_PEAK_GBPS,
                          path_algorithmic_gbps=s["path_gbps"], path_frac=s["path_gbps"] / HBM_PEAK_GBPS)
     in_kernel_coords = None
-    if not args.no_secondary:
+    if not args.no_secondary and not args.no_in_kernel_coords:
         # the same workload with the coordinate volume formed inside both kernels from the
         # per-frame cuboids instead of read from HBM
         k = run_config(args.config, args, rank, world, device, cuboid=True)

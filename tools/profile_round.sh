@@ -10,7 +10,7 @@ out=gpurun_out/$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o kt -- \
-    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$out/kt.log" 2>&1
+    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-in-kernel-coords > "$out/kt.log" 2>&1
 echo "kernel trace done"
 for cfg in 2 3; do
   for c in FETCH_SIZE WRITE_SIZE; do

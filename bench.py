@@ -135,8 +135,8 @@ class Workload:
         return sum(t) / len(t)
 
 
-def run_config(name, args, rank, world, device, cuboid=False):
-    cfg = CONFIGS[name]
+def run_config(name, args, rank, world, device, cuboid=False, cfg=None):
+    cfg = cfg if cfg is not None else CONFIGS[name]
     wl = Workload(cfg, rank, world, device, cuboid=cuboid)
     for _ in range(args.warmup):
         wl.step()
@@ -282,6 +282,17 @@ def main():
                                 unproject_achieved_gbps=k["achieved_gbps"],
                                 unproject_frac=k["achieved_gbps"] / HBM_PEAK_GBPS,
                                 path_algorithmic_gbps=k["path_gbps"])
+    cfg4 = None
+    if not args.no_secondary and args.config == "2":
+        # BASELINE config 4: 8 views, a global batch of 128 frames sharded over the ranks
+        # (strong scaling: 128 / world frames per GPU), joints all-gathered over RCCL
+        c4 = dict(CONFIGS["4"], frames=max(1, 128 // world))
+        r4 = run_config("4", args, rank, world, device, cfg=c4)
+        cfg4 = dict(workload=c4["label"] + ", global batch 128 sharded over the ranks", value=r4["fps"],
+                    unit="frames/s", scaling="strong", global_batch=c4["frames"] * world, frames_per_gpu=c4["frames"],
+                    ms_per_step=r4["ms_per_step"], unproject_ms=r4["unproject_ms"],
+                    unproject_achieved_gbps=r4["achieved_gbps"], unproject_frac=r4["achieved_gbps"] / HBM_PEAK_GBPS,
+                    path_algorithmic_gbps=r4["path_gbps"])
     cfg5 = None
     if not args.no_secondary and args.config == "2":
         cfg5 = run_config5(args, rank, world, device)
@@ -318,6 +329,7 @@ def main():
             "cpu_baseline": base,
             "secondary": secondary,
             "in_kernel_coords": in_kernel_coords,
+            "config4": cfg4,
             "config5": cfg5,
         }
         print(json.dumps(line), flush=True)

@@ -48,11 +48,21 @@ constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any
 // last 2 slots of each hold zeros: the taps of voxel-views that sample nothing point there).
 //   4 views: 4x8x16 tile, 512 threads, 2048 slots = 2 x 32 KiB (footprints of such tiles
 //            take ~2.2 slots / voxel)
-//   8 views: 2x8x16 tile, 256 threads, 2048 slots
+//   8 views: 4x8x16 tile, 512 threads, 4096 8-byte slots (2 channels) per buffer
 template <int NV> struct TileShape;
 // WAVES: waves per SIMD the register allocation must allow (4: two 512-thread blocks per CU).
-template <> struct TileShape<4> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, WAVES = 4; };
-template <> struct TileShape<8> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 4096, WAVES = 2; };
+template <> struct TileShape<4> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, G = 4, WAVES = 4; };
+// 8 views: 8-byte slots (2 channels) so that the two 4,096-slot buffers take 64 KiB and two
+// blocks share a CU (one block's prologue / barriers overlap the other's staging and
+// sampling): config 4 1,278 -> 1,027 us at 16 frames, bit-identical (A/B).
+// The 4-view kernel keeps 16-byte slots (2-channel slots at 6 waves/SIMD: no gain).
+#ifndef MVN_G_8VIEWS
+#define MVN_G_8VIEWS 2
+#endif
+template <> struct TileShape<8> {
+  static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 4096, G = MVN_G_8VIEWS;
+  static constexpr int WAVES = G == 2 ? 4 : 2;
+};
 
 // Wave-wide integer min / max, returned wave-uniform.  row_shr DPP steps (identity
 // shifted in) leave each row's reduction in its lane 15; four readlanes combine the rows.
@@ -98,14 +108,25 @@ template <> __device__ __forceinline__ void buf_store<uint16_t>(float x, __amdgp
   __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, 0);
 }
 
-// LDS slots hold 4 f32 channels whatever the input dtype: bf16 maps are widened once
-// when staged (each staged pixel is read ~7 times by the tile's taps), not per tap.
+// LDS slots hold G f32 channels whatever the input dtype (G = 4: 16-byte slots; G = 2:
+// 8-byte slots, half the LDS per block, so that two 8-view blocks share a CU): bf16 maps
+// are widened once when staged (each staged pixel is read ~7 times by the taps), not per tap.
+template <int G> struct SlotT;
+template <> struct SlotT<4> { using type = uint4; };
+template <> struct SlotT<2> { using type = uint2; };
 __device__ __forceinline__ void unpack(const uint4& q, float (&v)[4]) {
   v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+}
+__device__ __forceinline__ void unpack(const uint2& q, float (&v)[2]) {
+  v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y);
 }
 template <typename TIn> __device__ __forceinline__ uint4 pack(const uint32_t (&b)[4]) {
   if constexpr (sizeof(TIn) == 4) return make_uint4(b[0], b[1], b[2], b[3]);
   else return make_uint4(b[0] << 16, b[1] << 16, b[2] << 16, b[3] << 16);   // bf16 -> f32 bits
+}
+template <typename TIn> __device__ __forceinline__ uint2 pack(const uint32_t (&b)[2]) {
+  if constexpr (sizeof(TIn) == 4) return make_uint2(b[0], b[1]);
+  else return make_uint2(b[0] << 16, b[1] << 16);
 }
 
 // View aggregation, fast form for the staged path.  sum / max / conf are the reference's
@@ -202,11 +223,13 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ, kThreads = S::THREADS, kBuf = S::SLOTS;
   static_assert(TX * TY * TZ == kThreads, "one voxel per thread");
   constexpr int kWaves = kThreads / kWave;
-  constexpr int G = 4;                                // f32 channels per 16-byte LDS slot
+  constexpr int G = S::G;                             // f32 channels per LDS slot
+  using Slot = typename SlotT<G>::type;
+  constexpr uint32_t kSlotB = sizeof(Slot);
   constexpr int kZeroSlot = kBuf - 2;
   constexpr int MS = kBuf / kThreads;                 // staged slots per thread (max)
 
-  __shared__ uint4 stage[2 * kBuf];
+  __shared__ Slot stage[2 * kBuf];
   __shared__ int red[kWaves][NV][4];
   __shared__ int region[NV][6];                       // xs, ys, bw, pitch, first slot, end slot
   __shared__ int region_pass[NV];
@@ -240,7 +263,7 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
   const TIn* fb = feat + size_t(b) * N * C * HW;
   const float* cfb = conf ? conf + size_t(b) * N * C : nullptr;
 
-  if (t < 4) stage[(t >> 1) * kBuf + kZeroSlot + (t & 1)] = make_uint4(0, 0, 0, 0);
+  if (t < 4) stage[(t >> 1) * kBuf + kZeroSlot + (t & 1)] = Slot{};
 
   // ---- this thread's voxel -----------------------------------------------------------
   const int X = tx * TX + t / (TZ * TY), Y = ty * TY + (t / TZ) % TY, Z = tz * TZ + t % TZ;
@@ -359,8 +382,8 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int slot = rbase[v] + (fy[v] - ry[v]) * rpitch[v] + (fx[v] - rx[v]);
-    anw[v] = uint32_t(has[v] ? slot : kZeroSlot) * 16u;
-    asw[v] = uint32_t(has[v] ? slot + rpitch[v] : kZeroSlot) * 16u;
+    anw[v] = uint32_t(has[v] ? slot : kZeroSlot) * kSlotB;
+    asw[v] = uint32_t(has[v] ? slot + rpitch[v] : kZeroSlot) * kSlotB;
   }
 
   // sample the views staged in an LDS buffer (ONE_PASS: all of them; else those of `pass`)
@@ -371,10 +394,10 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
       if (!decltype(one_pass)::value && rpass[v] != pass) continue;
       // branch-free: voxel-views that sample nothing read the zero slots with zero weights
       float a[G], bq[G], cq[G], d[G];
-      unpack(*reinterpret_cast<const uint4*>(buf + anw[v]), a);
-      unpack(*reinterpret_cast<const uint4*>(buf + anw[v] + 16), bq);
-      unpack(*reinterpret_cast<const uint4*>(buf + asw[v]), cq);
-      unpack(*reinterpret_cast<const uint4*>(buf + asw[v] + 16), d);
+      unpack(*reinterpret_cast<const Slot*>(buf + anw[v]), a);
+      unpack(*reinterpret_cast<const Slot*>(buf + anw[v] + kSlotB), bq);
+      unpack(*reinterpret_cast<const Slot*>(buf + asw[v]), cq);
+      unpack(*reinterpret_cast<const Slot*>(buf + asw[v] + kSlotB), d);
 #pragma unroll
       for (int ch = 0; ch < G; ++ch)
         sv[ch][v] = __builtin_fmaf(d[ch], w[v][3], __builtin_fmaf(cq[ch], w[v][2],
@@ -391,7 +414,15 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
 #pragma unroll
       for (int ch = 0; ch < G; ++ch) r[ch] = aggregate_fast<AGG, NV>(sv[ch], N, cfb ? cfb + c0 + ch : nullptr, C);
       const uint32_t soff = uint32_t(c0) * uint32_t(sizeof(TOut));
-      if constexpr (sizeof(TOut) == 4) {
+      if constexpr (G == 2) {
+        if constexpr (sizeof(TOut) == 4)
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int,
+                                 make_uint2(__float_as_uint(r[0]), __float_as_uint(r[1]))),
+              ors, ooff_cl, soff, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(r[0], r[1]), ors, ooff_cl, soff, 0);
+      } else if constexpr (sizeof(TOut) == 4) {
         __builtin_amdgcn_raw_buffer_store_b128(
             __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
                                make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]),
@@ -443,12 +474,12 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
           for (int k = 0; k < G; ++k) pre[i][k] = buf_load<TIn>(frs, goff[i], uint32_t((c0 + k) * HW * int(sizeof(TIn))));
         }
     };
-    auto commit = [&](uint4* buf) __attribute__((always_inline)) {
+    auto commit = [&](Slot* buf) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < MS; ++i)
         if (UNCOND || wfirst + kThreads * i < total) buf[t + kThreads * i] = pack<TIn>(pre[i]);
     };
-    auto consume = [&](const uint4* buf, int c0) __attribute__((always_inline)) {
+    auto consume = [&](const Slot* buf, int c0) __attribute__((always_inline)) {
       float sv[G][NV];
       sample_views(reinterpret_cast<const char*>(buf), std::true_type{}, 0, sv);
       aggregate_store(c0, sv);

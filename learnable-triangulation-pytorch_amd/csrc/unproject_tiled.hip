@@ -37,8 +37,10 @@ namespace mvn {
 namespace unproj {
 namespace {
 
+// 4 views: skip, per wave, staged slots past the tile's footprint (A/B r04: 194.2 -> 191.1 us
+// at config 2, bit-identical); 8 views stage every slot a thread owns (1,031 vs 1,061 us).
 #ifndef MVN_STAGE_UNCOND
-#define MVN_STAGE_UNCOND 1   // stage every slot a thread owns (else skip slots past the footprint per wave)
+#define MVN_STAGE_UNCOND 0   // 1: stage every slot unconditionally for 4 views as well
 #endif
 
 constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any frame
@@ -465,7 +467,7 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
       goff[i] = in ? uint32_t((q.v * C * HW + gy * W + gx) * int(sizeof(TIn))) : kOob;
     }
     uint32_t pre[MS][G];
-    constexpr bool UNCOND = MVN_STAGE_UNCOND;
+    constexpr bool UNCOND = NV == 8 || MVN_STAGE_UNCOND;
     auto issue = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < MS; ++i)

@@ -167,7 +167,7 @@ def run_config(name, args, rank, world, device, cuboid=False, cfg=None):
         path_gbps=(frame_bytes_cuboid if cuboid else frame_bytes)(cfg, E) * frames_total / elapsed / 1e9)
 
 
-def run_config5(args, rank, world, device):
+def run_config5(args, rank, world, device, cuboid=False):
     """Config 5: unproject (softmax, written channels-last bf16) + V2V front block on MFMA;
     roofline of the front block against the bf16 dense MFMA peak."""
     from mvn_rocm import v2v
@@ -181,9 +181,10 @@ def run_config5(args, rank, world, device):
                                                   torch.randn(16, generator=g) * 0.1, torch.zeros(16), torch.ones(16),
                                                   device=device)
     ev = []
+    coords = vb.cuboids(device) if cuboid else vb.coords
 
     def step(timed=False):
-        cl = v2v.unproject_channels_last(vb.features, vb.proj, vb.coords, "softmax")
+        cl = v2v.unproject_channels_last(vb.features, vb.proj, coords, "softmax")
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -296,6 +297,9 @@ def main():
     cfg5 = None
     if not args.no_secondary and args.config == "2":
         cfg5 = run_config5(args, rank, world, device)
+        if not args.no_in_kernel_coords:
+            k5 = run_config5(args, rank, world, device, cuboid=True)
+            cfg5["in_kernel_coords"] = dict(value=k5["value"], unit="frames/s", ms_per_step=k5["ms_per_step"])
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base = cpu_baseline()

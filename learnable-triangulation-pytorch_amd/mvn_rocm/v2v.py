@@ -60,19 +60,34 @@ def v2v_front(vol_cl, packed, scale, shift, out_dtype=torch.float32):
 
 def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggregation_method="softmax",
                             out_dtype=torch.bfloat16, align_corners=False):
-    """unproject_heatmaps (op.py:99-163) written channels-last: (B, Vx, Vy, Vz, C)."""
+    """unproject_heatmaps (op.py:99-163) written channels-last: (B, Vx, Vy, Vz, C).
+    ``coord_volumes`` may be a ``volumetric.Cuboids`` (coordinates formed in-kernel)."""
     agg = aggregation_code(volume_aggregation_method)
     if agg == _lib.MVN_AGG_CONF:
         raise ValueError("unproject_channels_last: 'conf*' aggregation is not supported here")
     feat = heatmaps.contiguous()
     proj = proj_matricies.float().contiguous()
-    coords = coord_volumes.float().contiguous()
-    _require_gpu(feat, proj, coords)
-    B, N, C, H, W = feat.shape
-    Vx, Vy, Vz = coords.shape[1:4]
-    out = torch.empty((B, Vx, Vy, Vz, C), dtype=out_dtype, device=feat.device)
     fd = 0 if feat.dtype == torch.float32 else 1
     od = 0 if out_dtype == torch.float32 else 1
+    B, N, C, H, W = feat.shape
+    from .volumetric import Cuboids
+    if isinstance(coord_volumes, Cuboids) and N <= 8:
+        # coordinates formed in-kernel from the per-frame cuboids (bit-identical, DESIGN.md 4.5)
+        cub = coord_volumes
+        _require_gpu(feat, proj, cub.params)
+        V = cub.volume_size
+        out = torch.empty((B, V, V, V, C), dtype=out_dtype, device=feat.device)
+        code = _lib.load().mvn_unproject_cuboid(feat.data_ptr(), fd, proj.data_ptr(), cub.params.data_ptr(),
+                                                int(cub.transfer), None, out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC,
+                                                B, N, C, H, W, V, agg, int(align_corners), _stream(feat))
+        _lib.check(code, "mvn_unproject_cuboid")
+        return out
+    if isinstance(coord_volumes, Cuboids):
+        coord_volumes = coord_volumes.coord_volumes()
+    coords = coord_volumes.float().contiguous()
+    _require_gpu(feat, proj, coords)
+    Vx, Vy, Vz = coords.shape[1:4]
+    out = torch.empty((B, Vx, Vy, Vz, C), dtype=out_dtype, device=feat.device)
     code = _lib.load().mvn_unproject_ex(feat.data_ptr(), fd, proj.data_ptr(), coords.data_ptr(), None,
                                         out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC, B, N, C, H, W, Vx, Vy, Vz, agg,
                                         int(align_corners), _stream(feat))

@@ -131,3 +131,17 @@ def test_cuboid_gradients_match_the_volume_path(device):
     # the unprojection backward scatters with float atomics (csrc/unproject_bwd.hip): its
     # summation order, not the coordinates, varies between runs
     assert max_rel(grads[0].cpu().numpy(), grads[1].cpu().numpy()) <= 1e-5
+
+
+@pytest.mark.parametrize("dt", (torch.float32, torch.bfloat16))
+def test_channels_last_cuboid_is_bit_identical(device, dt):
+    """Config 5's channels-last unprojection (V2V front input) with in-kernel coordinates."""
+    from mvn_rocm import synth, v2v
+    B, V = 2, 32
+    vb = synth.volumetric_batch(B, n_views=4, channels=32, volume=8, seed=8)
+    cub, _ = _frames(B, V, seed=8)
+    feat, proj = vb.features.to(device).to(dt), vb.proj.to(device)
+    for od in ((torch.bfloat16, torch.float32) if dt == torch.bfloat16 else (torch.float32,)):
+        a = v2v.unproject_channels_last(feat, proj, cub, "softmax", out_dtype=od)
+        b = v2v.unproject_channels_last(feat, proj, cub.coord_volumes(), "softmax", out_dtype=od)
+        assert a.shape == (B, V, V, V, 32) and torch.equal(_bits(a), _bits(b))

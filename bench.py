@@ -7,20 +7,34 @@ over channels [0:17] of the unprojected volume (the stand-in for V2V, SURVEY.md 
 -> (N > 1) one all-gather of the (B/N, 17, 3) joints over RCCL.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--no-cpu-baseline]
+                    [--no-secondary] [--dry-run]
 
-With the default --config 2 the line also carries `secondary` (config 3, bf16, 32 frames)
-and `config5` (unproject written channels-last + the V2V front Conv3d block on bf16 MFMA,
-64 frames, with its own MFMA roofline); --no-secondary drops both.
+Process model (the reference's DDP model, /root/reference/train.py:370-382): one process
+per GPU.  Launched by torch.distributed.run (WORLD_SIZE set) every process is one rank.
+Launched as `python bench.py --gpus N` with no WORLD_SIZE, this process spawns the N rank
+processes itself (fresh interpreters with a torchrun-style environment, before anything
+here touches the GPU), waits for them and exits with their status.  Every rank builds
+its own frames from (seed, global frame index); the headline config is weak scaling
+(8 frames per GPU), config 4 is strong scaling (a global batch of 128 split over the
+ranks).  Rank 0 prints ONE JSON line.
 
-N > 1 is launched by torch.distributed.run (one process per GPU); every rank builds its
-own frames from (seed, global frame index) — weak scaling, fixed frames per GPU.
-Rank 0 prints ONE JSON line.
+--dry-run runs the whole multi-process protocol on the CPU (gloo): rank bring-up,
+barriers, max-over-ranks timing and the joints all-gather, with a stand-in step that
+needs no GPU (tests/test_bench.py).
+
+With the default --config 2 the line also carries `secondary` (config 3, bf16, 32 frames,
+with its own roofline block), `config1` (the algebraic path: DLT at batch 1, 4 views x 17
+joints, and the 2D soft-argmax -> DLT chain), `config4` and `config5` (unproject written
+channels-last + the V2V front Conv3d block on bf16 MFMA, 64 frames, MFMA roofline);
+--no-secondary drops them.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,48 +42,119 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "learnable-triangulation-pytorch_amd"))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-from mvn_rocm import dist as mdist, op, synth  # noqa: E402
-
 METRIC = "multiview frames/sec (4-view x 64^3 unproject+soft-argmax), 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-
-# BASELINE.json configs (per GPU): name -> (views, channels, heatmap, volume, joints, frames/GPU, dtype)
-CONFIGS = {
-    "2": dict(views=4, channels=32, heatmap=96, volume=64, joints=17, frames=8, dtype=torch.float32,
-              label="cfg2: 4 views x 32 ch x 96^2 -> 64^3 unproject(softmax agg) + 17-joint soft-argmax, fp32"),
-    "3": dict(views=4, channels=32, heatmap=96, volume=64, joints=17, frames=32, dtype=torch.bfloat16,
-              label="cfg3: 4 views x 32 ch x 96^2 -> 64^3 unproject(softmax agg) + 17-joint soft-argmax, bf16"),
-    "4": dict(views=8, channels=32, heatmap=96, volume=64, joints=17, frames=16, dtype=torch.float32,
-              label="cfg4: 8 views (CMU-style) x 32 ch x 96^2 -> 64^3 unproject + soft-argmax, fp32"),
-    "5": dict(views=4, channels=32, heatmap=96, volume=64, joints=17, frames=64, dtype=torch.bfloat16,
-              label="cfg5: 4 views x 32 ch x 96^2 -> 64^3 unproject(softmax agg, channels-last bf16) + V2V front "
-                    "Basic3DBlock(32,16,7) conv3d+BN+ReLU on bf16 MFMA"),
-}
-MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 (no sparsity)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 (no sparsity)
 V2V_FLOP_PER_FRAME = 2 * 32 * 16 * 343 * 64 ** 3
 
 
-def unproject_bytes(c, E):
+def _configs():
+    import torch
+    # BASELINE.json configs (per GPU): views, channels, heatmap, volume, joints, frames/GPU, dtype
+    return {
+        "2": dict(views=4, channels=32, heatmap=96, volume=64, joints=17, frames=8, dtype=torch.float32,
+                  label="cfg2: 4 views x 32 ch x 96^2 -> 64^3 unproject(softmax agg) + 17-joint soft-argmax, fp32"),
+        "3": dict(views=4, channels=32, heatmap=96, volume=64, joints=17, frames=32, dtype=torch.bfloat16,
+                  label="cfg3: 4 views x 32 ch x 96^2 -> 64^3 unproject(softmax agg) + 17-joint soft-argmax, bf16"),
+        "4": dict(views=8, channels=32, heatmap=96, volume=64, joints=17, frames=16, dtype=torch.float32,
+                  label="cfg4: 8 views (CMU-style) x 32 ch x 96^2 -> 64^3 unproject + soft-argmax, fp32"),
+        "5": dict(views=4, channels=32, heatmap=96, volume=64, joints=17, frames=64, dtype=torch.bfloat16,
+                  label="cfg5: 4 views x 32 ch x 96^2 -> 64^3 unproject(softmax agg, channels-last bf16) + V2V "
+                        "front Basic3DBlock(32,16,7) conv3d+BN+ReLU on bf16 MFMA"),
+    }
+
+
+# ----------------------------------------------------------------------------- process model
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """Spawn n rank processes of this script (torchrun-style environment, rendezvous on
+    127.0.0.1) and return the first non-zero exit status, or 0.  Called before anything in
+    this process touches the GPU; the ranks are fresh child processes, never an exec."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        if code != 0 and rc == 0:
+            rc = code
+            for q in procs:          # one rank failed: the others would block in a collective
+                if q.poll() is None:
+                    q.terminate()
+    return rc
+
+
+class Clock:
+    """Barrier + device sync around the timed region; max over ranks."""
+
+    def __init__(self, world, device, dry):
+        self.world, self.device, self.dry = world, device, dry
+
+    def sync(self):
+        import torch
+        if not self.dry:
+            torch.cuda.synchronize()
+
+    def fence(self):
+        import torch.distributed as dist
+        self.sync()
+        if self.world > 1:
+            dist.barrier()
+        self.sync()
+
+    def max_over_ranks(self, seconds):
+        import torch
+        import torch.distributed as dist
+        if self.world == 1:
+            return seconds
+        t = torch.tensor([seconds], device=self.device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def timed_loop(step, args, clock):
+    for _ in range(args.warmup):
+        step(False)
+    clock.fence()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    clock.fence()
+    return clock.max_over_ranks(time.perf_counter() - t0)
+
+
+# ----------------------------------------------------------------------------- algorithmic bytes
+def unproject_bytes(c, E, cuboid=False):
     """Algorithmic bytes of one frame's unprojection: features read once,
-    volume written once, coordinates read once (f32), projections read."""
+    volume written once, coordinates read once (f32; 18 floats of cuboid when formed
+    in-kernel), projections read."""
     V3 = c["volume"] ** 3
-    return E * (c["views"] * c["channels"] * c["heatmap"] ** 2 + c["channels"] * V3) + 4 * 3 * V3 + 4 * 12 * c["views"]
+    coords = 4 * 18 if cuboid else 4 * 3 * V3
+    return E * (c["views"] * c["channels"] * c["heatmap"] ** 2 + c["channels"] * V3) + coords + 4 * 12 * c["views"]
 
 
-def frame_bytes(c, E):
+def frame_bytes(c, E, cuboid=False):
     """Whole-path algorithmic bytes per frame (SURVEY.md §8d / BASELINE.md §4)."""
     V3 = c["volume"] ** 3
+    coords = 4 * 2 * 18 if cuboid else 4 * (2 * 3 * V3)
     return (E * (c["views"] * c["channels"] * c["heatmap"] ** 2 + c["channels"] * V3 + 2 * c["joints"] * V3)
-            + 4 * (2 * 3 * V3) + 4 * (12 * c["views"] + 3 * c["joints"]))
+            + coords + 4 * (12 * c["views"] + 3 * c["joints"]))
 
 
 def measured_traffic(cfg_name):
     """HBM bytes per unprojection launch from the newest committed PMC summary
-    (profiles/rNN_traffic.json, written by tools/profile_summary.py from rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes over the same kernel and config), or None."""
+    (profiles/rNN_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the
+    same kernel and config), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
     if not files:
@@ -82,96 +167,88 @@ def measured_traffic(cfg_name):
 
 
 def kernel_name(c):
+    import torch
     t = "float" if c["dtype"] == torch.float32 else "bf16"
     return f"unproject_tiled<softmax, {t}, {t}, {4 if c['views'] <= 4 else 8} views>"
 
 
 def dtype_name(dt):
+    import torch
     return {torch.float32: "f32", torch.bfloat16: "bf16"}[dt]
 
 
-def unproject_bytes_cuboid(c, E):
-    """Algorithmic bytes of one frame's unprojection with in-kernel coordinates: features
-    read once, volume written once, cuboid (18 f32) and projections read."""
-    V3 = c["volume"] ** 3
-    return E * (c["views"] * c["channels"] * c["heatmap"] ** 2 + c["channels"] * V3) + 4 * 18 + 4 * 12 * c["views"]
+def roofline(c, r, cfg_name):
+    traffic, src = measured_traffic(cfg_name)
+    return {"kernel": kernel_name(c), "bound": "hbm", "achieved": r["achieved_gbps"], "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": r["achieved_gbps"] / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": src,
+            "launch_ms": r["unproject_ms"], "algorithmic_bytes_per_launch": r["launch_bytes"]}
 
 
-def frame_bytes_cuboid(c, E):
-    V3 = c["volume"] ** 3
-    return (E * (c["views"] * c["channels"] * c["heatmap"] ** 2 + c["channels"] * V3 + 2 * c["joints"] * V3)
-            + 4 * 2 * 18 + 4 * (12 * c["views"] + 3 * c["joints"]))
-
-
+# ----------------------------------------------------------------------------- workloads
 class Workload:
-    def __init__(self, cfg, rank, world, device, seed=0, cuboid=False):
-        self.cfg, self.rank, self.world, self.device = cfg, rank, world, device
+    """One rank's frames of a config, resident on the device, and the timed step."""
+
+    def __init__(self, cfg, rank, world, device, seed=0, cuboid=False, first_frame=None):
+        import torch
+        from mvn_rocm import synth
+        self.cfg, self.world, self.device = cfg, world, device
         B = cfg["frames"]
+        self.global_batch = B * world
+        first = rank * B if first_frame is None else first_frame
         vb = synth.volumetric_batch(B, n_views=cfg["views"], channels=cfg["channels"], heatmap=cfg["heatmap"],
                                     volume=cfg["volume"], dtype=cfg["dtype"], device=device, seed=seed,
-                                    first_frame=rank * B)
+                                    first_frame=first)
         self.feat, self.proj, self.coords = vb.features, vb.proj, vb.coords
         if cuboid:      # coordinates formed inside both kernels (mvn_*_cuboid), never materialised
             self.coords = vb.cuboids(device)
         self.ev = []
+        self._event = lambda: torch.cuda.Event(enable_timing=True)
 
     def step(self, timed=False):
+        from mvn_rocm import dist as mdist, op
         J = self.cfg["joints"]
         if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0, e1, e2 = self._event(), self._event(), self._event()
             e0.record()
         vol = op.unproject_heatmaps(self.feat, self.proj, self.coords, "softmax")
         if timed:
             e1.record()
-            self.ev.append((e0, e1))
         xyz, sm = op.integrate_tensor_3d_with_coordinates(vol[:, :J], self.coords, True)
+        if timed:
+            e2.record()
+            self.ev.append((e0, e1, e2))
         if self.world > 1:      # the path's one exchange: joints of every rank, RCCL over xGMI
-            xyz = mdist.gather_joints(xyz, self.cfg["frames"] * self.world)
+            xyz = mdist.gather_joints(xyz, self.global_batch)
         return xyz, sm
 
-    def unproject_ms(self):
+    def kernel_ms(self):
+        import torch
         torch.cuda.synchronize()
-        t = [a.elapsed_time(b) for a, b in self.ev]
-        return sum(t) / len(t)
+        n = len(self.ev)
+        return (sum(a.elapsed_time(b) for a, b, _ in self.ev) / n, sum(b.elapsed_time(c) for _, b, c in self.ev) / n)
 
 
-def run_config(name, args, rank, world, device, cuboid=False, cfg=None):
-    cfg = cfg if cfg is not None else CONFIGS[name]
-    wl = Workload(cfg, rank, world, device, cuboid=cuboid)
-    for _ in range(args.warmup):
-        wl.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        wl.step(timed=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+def run_config(name, args, rank, world, device, clock, cuboid=False, cfg=None, first_frame=None):
+    import torch
+    cfg = cfg if cfg is not None else _configs()[name]
+    wl = Workload(cfg, rank, world, device, cuboid=cuboid, first_frame=first_frame)
+    elapsed = timed_loop(lambda t: wl.step(t), args, clock)
     E = 2 if cfg["dtype"] == torch.bfloat16 else 4
-    frames_total = cfg["frames"] * world * args.steps
-    unproj_ms = wl.unproject_ms()
-    launch_bytes = (unproject_bytes_cuboid if cuboid else unproject_bytes)(cfg, E) * cfg["frames"]
-    achieved = launch_bytes / (unproj_ms * 1e-3) / 1e9
-    return dict(
-        cfg=cfg, elapsed=elapsed, fps=frames_total / elapsed, ms_per_step=elapsed / args.steps * 1e3,
-        unproject_ms=unproj_ms, launch_bytes=launch_bytes, achieved_gbps=achieved,
-        path_gbps=(frame_bytes_cuboid if cuboid else frame_bytes)(cfg, E) * frames_total / elapsed / 1e9)
+    frames_total = wl.global_batch * args.steps
+    unproj_ms, sa_ms = wl.kernel_ms()
+    launch_bytes = unproject_bytes(cfg, E, cuboid) * cfg["frames"]
+    return dict(cfg=cfg, elapsed=elapsed, fps=frames_total / elapsed, ms_per_step=elapsed / args.steps * 1e3,
+                unproject_ms=unproj_ms, softargmax_ms=sa_ms, launch_bytes=launch_bytes,
+                achieved_gbps=launch_bytes / (unproj_ms * 1e-3) / 1e9,
+                path_gbps=frame_bytes(cfg, E, cuboid) * frames_total / elapsed / 1e9)
 
 
-def run_config5(args, rank, world, device, cuboid=False):
+def run_config5(args, rank, world, device, clock, cuboid=False):
     """Config 5: unproject (softmax, written channels-last bf16) + V2V front block on MFMA;
     roofline of the front block against the bf16 dense MFMA peak."""
-    from mvn_rocm import v2v
-    cfg = CONFIGS["5"]
+    import torch
+    from mvn_rocm import synth, v2v
+    cfg = _configs()["5"]
     B = cfg["frames"]
     vb = synth.volumetric_batch(B, n_views=cfg["views"], channels=cfg["channels"], heatmap=cfg["heatmap"],
                                 volume=cfg["volume"], dtype=cfg["dtype"], device=device, seed=0, first_frame=rank * B)
@@ -194,24 +271,7 @@ def run_config5(args, rank, world, device, cuboid=False):
             ev.append((e0, e1))
         return y
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(timed=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_loop(step, args, clock)
     conv_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     tflops = V2V_FLOP_PER_FRAME * B / (conv_ms * 1e-3) / 1e12
     return dict(workload=cfg["label"], value=B * world * args.steps / elapsed, unit="frames/s",
@@ -222,91 +282,229 @@ def run_config5(args, rank, world, device, cuboid=False):
                           "flop_per_launch": V2V_FLOP_PER_FRAME * B})
 
 
-def cpu_baseline(seconds=15.0):
-    """The reference algorithm restated op-for-op in torch-CPU (oracle/restate_torch.py),
-    timed on this host on one frame of config 2 at a time (bounded sample)."""
-    from oracle import restate_torch
+def run_config1(args, device):
+    """BASELINE config 1, the algebraic path at batch 1 (4 views x 17 joints): the DLT alone
+    (triangulate_batch_of_points, multiview.py:162-174) and the model's chain from heatmaps
+    (triangulation.py:164-191): 2D soft-argmax of heatmaps * 100 -> confidence
+    normalisation -> upscale to image pixels -> DLT.  Device time from HIP events around
+    100 back-to-back calls; wall time per call includes the host launch."""
+    import torch
+    from mvn_rocm import multiview, op, synth
+    ab = synth.algebraic_batch(1, 4, 17, seed=0)
+    P, pts, conf = ab.proj.to(device), ab.points.to(device), ab.confidences.to(device)
+    hm = torch.randn((4, 17, 96, 96), generator=torch.Generator().manual_seed(1)).to(device)
+    raw_conf = torch.rand((1, 4, 17), generator=torch.Generator().manual_seed(2)).to(device) + 0.1
+
+    def dlt():
+        return multiview.triangulate_batch_of_points(P, pts, conf)
+
+    def chain():
+        xy, _ = op.integrate_tensor_2d(hm, True, multiplier=100.0, return_heatmaps=False)
+        xy = xy.view(1, 4, 17, 2) * 4.0                      # 384 / 96, both axes
+        c = raw_conf / raw_conf.sum(dim=1, keepdim=True) + 1e-5
+        return multiview.triangulate_batch_of_points(P, xy, c)
+
+    res = {}
+    for name, fn in (("dlt", dlt), ("chain", chain)):
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n = max(100, args.steps)
+        t0 = time.perf_counter()
+        e0.record()
+        for _ in range(n):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        res[name] = (e0.elapsed_time(e1) / n * 1e3, (time.perf_counter() - t0) / n * 1e6)
+    return dict(workload="cfg1: algebraic DLT (triangulate_batch_of_points), 4 views x 17 joints, batch 1, f32 in, "
+                         "f64 null-vector solve",
+                dlt_device_us=res["dlt"][0], dlt_wall_us=res["dlt"][1], value=1e6 / res["dlt"][1],
+                unit="frames/s (batch 1, host-launch inclusive)",
+                chain_workload="integrate_tensor_2d(heatmaps x100, 4x17x96^2) -> conf norm -> upscale -> DLT",
+                chain_device_us=res["chain"][0], chain_wall_us=res["chain"][1])
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def _host_cores():
+    """(physical cores, logical CPUs) of the host from lscpu, or (None, os.cpu_count())."""
+    try:
+        out = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+        cores = {ln for ln in out.splitlines() if ln and not ln.startswith("#")}
+        return (len(cores) or None), os.cpu_count()
+    except (OSError, subprocess.SubprocessError):
+        return None, os.cpu_count()
+
+
+def cpu_baseline(budget_s=8.0):
+    """The reference algorithm restated op-for-op in torch-CPU (oracle/restate_torch.py,
+    pinned bit-exact to the reference by tests/test_oracle.py), timed on this host at the
+    config-2 batch of 8 frames: with every thread torch uses here, and with one thread;
+    plus config 1 (DLT, batch 1).  Bounded sample: whole batches until `budget_s` per leg."""
     import warnings
+
+    import torch
+    from mvn_rocm import synth
+    from oracle import restate_torch
     warnings.filterwarnings("ignore")
-    vb = synth.volumetric_batch(1, seed=0)
-    cfg = CONFIGS["2"]
-    n, t0 = 0, time.perf_counter()
-    while True:
-        vol = restate_torch.unproject_heatmaps(vb.features, vb.proj, vb.coords, "softmax")
-        restate_torch.integrate_tensor_3d_with_coordinates(vol[:, :cfg["joints"]], vb.coords, True)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 50:
-            break
-    return dict(value=n / el, unit="frames/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"{n} frame(s) of config 2 (4x32x96^2 -> 64^3, softmax agg, 17-joint soft-argmax, fp32) "
-                       f"through oracle/restate_torch.py in {el:.1f} s")
+    cfg = _configs()["2"]
+    vb = synth.volumetric_batch(cfg["frames"], seed=0)
+
+    def batches(budget):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            vol = restate_torch.unproject_heatmaps(vb.features, vb.proj, vb.coords, "softmax")
+            restate_torch.integrate_tensor_3d_with_coordinates(vol[:, :cfg["joints"]], vb.coords, True)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return n, el
+
+    threads = torch.get_num_threads()
+    n_all, el_all = batches(budget_s)
+    torch.set_num_threads(1)
+    n_one, el_one = batches(0.0)                     # one batch (~8x the all-thread time)
+    ab = synth.algebraic_batch(1, 4, 17, seed=0)
+    nd, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 1.0:
+        restate_torch.triangulate_batch_of_points(ab.proj, ab.points, ab.confidences)
+        nd += 1
+    dlt_ms = (time.perf_counter() - t0) / nd * 1e3
+    torch.set_num_threads(threads)
+    phys, logical = _host_cores()
+    B = cfg["frames"]
+    return dict(value=n_all * B / el_all, unit="frames/s", cores=threads, kind="port",
+                sample=f"{n_all} batch(es) of {B} frames of config 2 (4x32x96^2 -> 64^3, softmax agg, 17-joint "
+                       f"soft-argmax, fp32) through oracle/restate_torch.py (op-for-op restatement of "
+                       f"op.py:84-163, bit-exact with the reference) in {el_all:.1f} s, {threads} threads",
+                threads_1=dict(value=n_one * B / el_one, unit="frames/s", cores=1,
+                               sample=f"{n_one} batch(es) of {B} frames in {el_one:.1f} s, 1 thread"),
+                host_physical_cores=phys, host_logical_cpus=logical,
+                config1_dlt_ms_per_frame=dlt_ms,
+                config1_sample=f"{nd} calls of restate_torch.triangulate_batch_of_points (multiview.py:132-174), "
+                               f"batch 1, 4 views x 17 joints, {threads} threads")
 
 
+# ----------------------------------------------------------------------------- dry run (CPU)
+def dry_run(args, rank, world):
+    """The multi-rank protocol of the bench on the CPU (gloo): every rank builds its own
+    frames of a miniature config-2 batch from (seed, global frame index), a stand-in step
+    (the mean of each frame's coordinate volume as 17 'joints') and the joints all-gather;
+    rank 0 checks the gathered joints against all frames built locally."""
+    import torch
+    from mvn_rocm import dist as mdist, synth
+    B = 8
+    G = B * world
+
+    def joints(first, count):
+        vb = synth.volumetric_batch(count, n_views=4, channels=1, heatmap=8, volume=4, seed=0, first_frame=first)
+        return vb.coords.reshape(count, -1, 3).mean(1, keepdim=True).expand(count, 17, 3).contiguous()
+
+    local = joints(rank * B, B)
+    clock = Clock(world, torch.device("cpu"), True)
+
+    def step(_timed):
+        return mdist.gather_joints(local, G) if world > 1 else local
+
+    elapsed = timed_loop(step, args, clock)
+    got = step(False)
+    ok = bool(torch.equal(got, joints(0, G))) if rank == 0 else None
+    return dict(metric=METRIC, value=G * args.steps / elapsed, unit="frames/s", n_gpus=world, steps=args.steps,
+                warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True, scaling="weak",
+                vs_baseline=None, dtype="f32", data="dry run: CPU/gloo protocol check, stand-in step (no HIP)",
+                dry_run=True, gather_verified=ok,
+                config={"workload": "dry run of the config-2 sharding", "global_batch": G, "frames_per_gpu": B,
+                        "parallelism": f"dp{world}", "collective": "all_gather joints (gloo)" if world > 1 else None})
+
+
+# ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="2", choices=[k for k in sorted(CONFIGS) if k != "5"])
+    ap.add_argument("--config", default="2", choices=["2", "3", "4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-in-kernel-coords", action="store_true",
                     help="skip the in-kernel-coordinates run (keeps rocprof kernel means per variant clean)")
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo protocol check, no GPU")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        line = dry_run(args, rank, world)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
+    clock = Clock(world, device, False)
+    configs = _configs()
+    extras = not args.no_secondary and args.config == "2"
 
-    main_res = run_config(args.config, args, rank, world, device)
-    secondary = None
-    if not args.no_secondary and args.config == "2":
-        s = run_config("3", args, rank, world, device)
+    main_res = run_config(args.config, args, rank, world, device, clock)
+    secondary = config1 = in_kernel_coords = cfg4 = cfg5 = None
+    if extras:
+        s = run_config("3", args, rank, world, device, clock)
         secondary = dict(workload=s["cfg"]["label"], value=s["fps"], unit="frames/s", ms_per_step=s["ms_per_step"],
-                         frames_per_gpu=s["cfg"]["frames"], unproject_ms=s["unproject_ms"],
-                         unproject_achieved_gbps=s["achieved_gbps"],
-                         unproject_frac=s["achieved_gbps"] / HBM_PEAK_GBPS,
+                         frames_per_gpu=s["cfg"]["frames"], dtype="bf16", unproject_ms=s["unproject_ms"],
+                         softargmax_ms=s["softargmax_ms"], roofline=roofline(s["cfg"], s, "3"),
                          path_algorithmic_gbps=s["path_gbps"], path_frac=s["path_gbps"] / HBM_PEAK_GBPS)
-    in_kernel_coords = None
     if not args.no_secondary and not args.no_in_kernel_coords:
         # the same workload with the coordinate volume formed inside both kernels from the
         # per-frame cuboids (SURVEY.md §8f rank 2) instead of read from HBM
-        k = run_config(args.config, args, rank, world, device, cuboid=True)
+        k = run_config(args.config, args, rank, world, device, clock, cuboid=True)
         in_kernel_coords = dict(workload=k["cfg"]["label"] + ", coordinates formed in-kernel from per-frame cuboids",
                                 value=k["fps"], unit="frames/s", ms_per_step=k["ms_per_step"],
                                 unproject_ms=k["unproject_ms"], unproject_algorithmic_bytes_per_launch=k["launch_bytes"],
                                 unproject_achieved_gbps=k["achieved_gbps"],
                                 unproject_frac=k["achieved_gbps"] / HBM_PEAK_GBPS,
                                 path_algorithmic_gbps=k["path_gbps"])
-    cfg4 = None
-    if not args.no_secondary and args.config == "2":
-        # BASELINE config 4: 8 views, a global batch of 128 frames sharded over the ranks
-        # (strong scaling: 128 / world frames per GPU), joints all-gathered over RCCL
-        c4 = dict(CONFIGS["4"], frames=max(1, 128 // world))
-        r4 = run_config("4", args, rank, world, device, cfg=c4)
-        cfg4 = dict(workload=c4["label"] + ", global batch 128 sharded over the ranks", value=r4["fps"],
-                    unit="frames/s", scaling="strong", global_batch=c4["frames"] * world, frames_per_gpu=c4["frames"],
+    if extras:
+        # BASELINE config 4: 8 views, a global batch of 128 frames split over the ranks
+        # (strong scaling), joints all-gathered over RCCL inside the timed step
+        from mvn_rocm import dist as mdist
+        start, count = mdist.shard(128, world, rank)
+        c4 = dict(configs["4"], frames=count)
+        r4 = run_config("4", args, rank, world, device, clock, cfg=c4, first_frame=start)
+        cfg4 = dict(workload=c4["label"] + ", global batch 128 split over the ranks", value=128 * args.steps / r4["elapsed"],
+                    unit="frames/s", scaling="strong", global_batch=128, frames_per_gpu=count,
                     ms_per_step=r4["ms_per_step"], unproject_ms=r4["unproject_ms"],
                     unproject_achieved_gbps=r4["achieved_gbps"], unproject_frac=r4["achieved_gbps"] / HBM_PEAK_GBPS,
-                    path_algorithmic_gbps=r4["path_gbps"])
-    cfg5 = None
-    if not args.no_secondary and args.config == "2":
-        cfg5 = run_config5(args, rank, world, device)
+                    collective="all_gather joints (RCCL)" if world > 1 else None)
+        cfg5 = run_config5(args, rank, world, device, clock)
         if not args.no_in_kernel_coords:
-            k5 = run_config5(args, rank, world, device, cuboid=True)
+            k5 = run_config5(args, rank, world, device, clock, cuboid=True)
             cfg5["in_kernel_coords"] = dict(value=k5["value"], unit="frames/s", ms_per_step=k5["ms_per_step"])
+        if rank == 0:
+            config1 = run_config1(args, device)
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base = cpu_baseline()
 
     if rank == 0:
         r, c = main_res, main_res["cfg"]
-        traffic, traffic_src = measured_traffic(args.config)
         line = {
             "metric": METRIC,
             "value": r["fps"],
@@ -324,14 +522,12 @@ def main():
                        "views": c["views"], "channels": c["channels"], "heatmap": c["heatmap"],
                        "volume": c["volume"], "joints": c["joints"], "parallelism": f"dp{world}",
                        "collective": "all_gather joints (RCCL)" if world > 1 else None},
-            "roofline": {"kernel": kernel_name(c), "bound": "hbm",
-                         "achieved": r["achieved_gbps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": r["achieved_gbps"] / HBM_PEAK_GBPS, "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "launch_ms": r["unproject_ms"], "algorithmic_bytes_per_launch": r["launch_bytes"]},
+            "roofline": roofline(c, r, args.config),
+            "softargmax_ms": r["softargmax_ms"],
             "path_algorithmic_gbps": r["path_gbps"],
             "cpu_baseline": base,
             "secondary": secondary,
+            "config1": config1,
             "in_kernel_coords": in_kernel_coords,
             "config4": cfg4,
             "config5": cfg5,

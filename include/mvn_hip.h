@@ -32,7 +32,8 @@
  *     hipGraph.
  *   - Return value: MVN_OK (0) or a negative MVN_ERR_* code.  Argument checks run
  *     before any HIP call, so they are safe without a GPU.
- *   - Functions are reentrant; the library keeps no mutable global state.
+ *   - Functions are reentrant; the library keeps no mutable global state apart from
+ *     the test-only knobs of mvn_debug_set_unproject (atomics).
  */
 #ifndef MVN_HIP_H
 #define MVN_HIP_H
@@ -204,8 +205,9 @@ int mvn_softargmax3d_cuboid(const void* vol, int vol_dtype,
                             int B, int J, int V, void* stream);
 
 /*
- * Nearest voxel per (frame, joint): argmin over the V^3 voxels of the f32 squared distance
- * between coords[b] (B, Vx, Vy, Vz, 3) and keypoints (B, J, 3); first index on ties.
+ * Nearest voxel per (frame, joint): argmin over the V^3 voxels of the f32 distance
+ * sqrt(((c - k)^2).sum(-1)) between coords[b] (B, Vx, Vy, Vz, 3) and keypoints (B, J, 3),
+ * IEEE square root, first index on ties (torch.argmin).
  *   out_index (B, J) int32, flat row-major voxel index (VolumetricCELoss, loss.py:63-67).
  */
 int mvn_nearest_voxel(const float* coords, const float* keypoints, int* out_index, int B, int J,
@@ -252,6 +254,15 @@ int mvn_softargmax3d_backward(const void* vol, int vol_dtype, int64_t vol_bstrid
  */
 int mvn_dlt_backward(const float* proj, const float* pts, const float* conf, const float* grad_out,
                      float* grad_pts, float* grad_conf, int B, int N, int J, void* stream);
+
+/*
+ * Test hook (tests only; process-wide, thread-safe): force unprojection code paths.
+ *   lds_slots  > 0: LDS slot budget per staging pass of the tiled kernel (small budgets
+ *              force the multi-pass and global-gather paths); 0 = the kernel's own budget
+ *   kernel     0 = default dispatch, 1 = the simple register-geometry kernel
+ * Returns MVN_OK, or MVN_ERR_ARG for a negative budget or an unknown kernel.
+ */
+int mvn_debug_set_unproject(int lds_slots, int kernel);
 
 #ifdef __cplusplus
 }

@@ -3,13 +3,10 @@
 //
 // Replaces the distance volume + torch.argmin of mvn/models/loss.py:63-67
 // (VolumetricCELoss): for every (frame, joint) the index of the voxel whose coordinate is
-// closest to the ground-truth keypoint.  The reference takes the argmin of
-// sqrt(sum((c - k)^2)) with the sum in sequence over x, y, z (f32, verified) and the
-// FIRST minimal index; here the argmin of the same f32 squared sum, first index on ties.
-// sqrt is monotonic, so the two agree except where the reference's rounded square roots
-// tie two distinct squared distances (the nearest voxel is ~1 voxel pitch closer than the
-// next, so this does not occur on real grids; tests check the golden's gradients, which
-// are non-zero exactly at the reference's argmin voxels).
+// closest to the ground-truth keypoint.  Same rule as the reference: the f32 squared
+// distance summed in sequence over x, y, z (verified), its square root (IEEE, correctly
+// rounded: torch.sqrt on the GPU; numpy), and the FIRST index among equal roots — two
+// distinct squared distances whose roots round to one f32 value tie, as in torch.argmin.
 // One 256-thread block per (frame, joint); the coordinate volume is read once per joint
 // (L2-resident across the joints of a frame).  Output: int32 flat voxel index.
 #include <climits>
@@ -37,8 +34,8 @@ __global__ __launch_bounds__(kBlock) void nearest_voxel(const float* __restrict_
   int bi = INT_MAX;
   for (int i = t; i < nvox; i += kBlock) {
     const float dx = c[size_t(i) * 3] - kx, dy = c[size_t(i) * 3 + 1] - ky, dz = c[size_t(i) * 3 + 2] - kz;
-    const float d = (dx * dx + dy * dy) + dz * dz;   // loss.py:63, summed x, y, z in order
-    better(best, bi, d, i);
+    const float d2 = (dx * dx + dy * dy) + dz * dz;  // loss.py:63, summed x, y, z in order
+    better(best, bi, sqrtf(d2), i);   // sqrtf: correctly rounded (v_sqrt + fma correction)
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) better(best, bi, __shfl_xor(best, o, kWave), __shfl_xor(bi, o, kWave));

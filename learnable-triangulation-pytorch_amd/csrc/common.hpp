@@ -74,6 +74,12 @@ __device__ __forceinline__ void cuboid_coord(const float* __restrict__ cub, int 
 
 inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
 
+// Test-only knobs of the unprojection dispatch (mvn_debug_set_unproject, unproject.hip):
+// process-wide atomics set by tests to force the multi-pass / global-gather / simple
+// kernel paths; nothing is read from the environment on the launch path.
+int unproject_lds_slot_budget();   // 0 = the kernel's own budget
+bool unproject_force_simple();
+
 // XCD-aware block order (cdna_hip_programming.md §5.5 T1, bijective form): hardware deals
 // blocks round-robin over the 8 XCDs, so block b runs on XCD b % 8.  Remapping gives each
 // XCD one contiguous range of logical work items, which keeps a frame's feature maps in

@@ -16,6 +16,8 @@
 // 'softmax' differs only by exp() rounding (<= 1e-6 rel).
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "unproject_common.hpp"
 
 namespace mvn {
@@ -129,12 +131,9 @@ __global__ __launch_bounds__(kUnprojBlock) void unproject_anyviews(
 }
 
 // Kernel choice: the tiled LDS-staged kernel (unproject_tiled.hip) for N <= 8 views, the
-// register-geometry kernel above for MVN_UNPROJECT_KERNEL=simple (A/B and debugging), and
-// the any-N kernel for more than 8 views.
-inline bool use_simple_kernel() {
-  const char* e = getenv("MVN_UNPROJECT_KERNEL");
-  return e && e[0] == 's';
-}
+// register-geometry kernel above when a test forces it (mvn_debug_set_unproject), and the
+// any-N kernel for more than 8 views.
+inline bool use_simple_kernel() { return unproject_force_simple(); }
 
 template <int AGG, typename TIn, typename TOut>
 int launch_agg(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
@@ -207,6 +206,21 @@ int unproject_entry(const void* feat, int feat_dtype, const float* proj, const f
 }
 }  // namespace
 }  // namespace mvn
+
+namespace mvn {
+namespace {
+std::atomic<int> g_lds_slots{0}, g_force_simple{0};
+}  // namespace
+int unproject_lds_slot_budget() { return g_lds_slots.load(std::memory_order_relaxed); }
+bool unproject_force_simple() { return g_force_simple.load(std::memory_order_relaxed) != 0; }
+}  // namespace mvn
+
+extern "C" int mvn_debug_set_unproject(int lds_slots, int kernel) {
+  if (lds_slots < 0 || (kernel != 0 && kernel != 1)) return MVN_ERR_ARG;
+  mvn::g_lds_slots.store(lds_slots, std::memory_order_relaxed);
+  mvn::g_force_simple.store(kernel, std::memory_order_relaxed);
+  return MVN_OK;
+}
 
 extern "C" int mvn_unproject_ex(const void* feat, int feat_dtype, const float* proj, const float* coords,
                                 const float* conf, void* out, int out_dtype, int out_layout, int B, int N, int C,

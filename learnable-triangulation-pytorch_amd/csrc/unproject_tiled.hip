@@ -26,8 +26,6 @@
 // Footprints that do not fit one LDS buffer together are staged in several passes
 // (slower, unpipelined); a single footprint larger than a whole buffer (a camera inside
 // the cuboid) sends its block to direct global gathers.
-#include <stdlib.h>
-
 #include <climits>
 #include <utility>
 
@@ -546,10 +544,10 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
   if ((long long)N * C * H * W * sizeof(TIn) >= (1LL << 31) ||
       (long long)C * Vx * Vy * Vz * sizeof(TOut) >= (1LL << 31))
     return MVN_ERR_SHAPE;
-  // LDS slot budget per pass (clamped in-kernel to the buffer); MVN_UNPROJECT_LDS_SLOTS
-  // lowers it (tests force the multi-pass and global-gather paths with it).
-  int budget = 1 << 30;
-  if (const char* e = getenv("MVN_UNPROJECT_LDS_SLOTS")) budget = max(1, atoi(e));
+  // LDS slot budget per pass (clamped in-kernel to the buffer); tests lower it through
+  // mvn_debug_set_unproject to force the multi-pass and global-gather paths.
+  const int knob = unproject_lds_slot_budget();
+  const int budget = knob > 0 ? knob : 1 << 30;
   auto go = [&](auto nv, auto exact) {
     constexpr int NV = decltype(nv)::value;
     using S = TileShape<NV>;

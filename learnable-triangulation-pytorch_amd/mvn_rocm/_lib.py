@@ -52,6 +52,7 @@ SIGNATURES = {
                                            _c_void_p, _c_void_p, _c_int, _c_void_p, _c_int, _c_void_p, _c_size_t]
                                   + [_c_int] * 5 + [_c_void_p]),
     "mvn_dlt_backward": (_c_int, [_c_void_p] * 6 + [_c_int, _c_int, _c_int, _c_void_p]),
+    "mvn_debug_set_unproject": (_c_int, [_c_int, _c_int]),
 }
 
 _lib = None
@@ -83,3 +84,19 @@ def check(code: int, what: str) -> None:
     if code != MVN_OK:
         msg = load().mvn_strerror(code).decode()
         raise MvnError(f"{what}: {msg} (code {code})")
+
+
+class unproject_knobs:
+    """Context manager (tests only): force unprojection paths through the C ABI's test hook
+    ``mvn_debug_set_unproject`` and restore the defaults on exit."""
+
+    def __init__(self, lds_slots: int = 0, simple: bool = False):
+        self.args = (int(lds_slots), int(bool(simple)))
+
+    def __enter__(self):
+        check(load().mvn_debug_set_unproject(*self.args), "mvn_debug_set_unproject")
+        return self
+
+    def __exit__(self, *exc):
+        check(load().mvn_debug_set_unproject(0, 0), "mvn_debug_set_unproject")
+        return False

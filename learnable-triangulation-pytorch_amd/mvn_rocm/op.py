@@ -36,6 +36,29 @@ def _dtype_code(dtype: torch.dtype) -> int:
     raise TypeError(f"mvn_rocm supports float32 and bfloat16, got {dtype}")
 
 
+def unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, method, cuboids=None):
+    """Checked, contiguous (features, projections, confidences-or-None) of an unprojection
+    call (shared by every unprojection entry point): features cast to float32 unless they
+    are float32 / bfloat16 (op.py:99 takes any float tensor), projections (B, N, 3, 4),
+    confidences (B, N, C) for 'conf*' only, and a ``Cuboids`` — when given — for B frames."""
+    if agg == _lib.MVN_AGG_CONF and vol_confidences is None:
+        raise TypeError("volume_aggregation_method '{}' needs vol_confidences".format(method))
+    feat = heatmaps.contiguous()
+    if feat.dtype not in (torch.float32, torch.bfloat16):
+        feat = feat.float()
+    if feat.dim() != 5:
+        raise RuntimeError(f"heatmaps must be (B, N, C, H, W), got {tuple(feat.shape)}")
+    proj = proj_matricies.float().contiguous()
+    conf = vol_confidences.float().contiguous() if agg == _lib.MVN_AGG_CONF else None
+    if proj.shape[:2] != feat.shape[:2] or proj.shape[2:] != (3, 4):
+        raise RuntimeError(f"proj_matricies shape {tuple(proj.shape)} does not match heatmaps {tuple(feat.shape)}")
+    if conf is not None and conf.shape != feat.shape[:3]:
+        raise RuntimeError(f"vol_confidences must be {tuple(feat.shape[:3])}, got {tuple(conf.shape)}")
+    if cuboids is not None and cuboids.batch != feat.shape[0]:
+        raise RuntimeError(f"cuboids for {cuboids.batch} frames, heatmaps have {feat.shape[0]}")
+    return feat, proj, conf
+
+
 def unproject_heatmaps(heatmaps, proj_matricies, coord_volumes, volume_aggregation_method='sum',
                        vol_confidences=None, *, align_corners=False, out_dtype=None):
     """Lift N views of C-channel maps into a (B, C, Vx, Vy, Vz) volume.
@@ -49,21 +72,9 @@ def unproject_heatmaps(heatmaps, proj_matricies, coord_volumes, volume_aggregati
     """
     agg = aggregation_code(volume_aggregation_method)
     cub = coord_volumes if _is_cuboids(coord_volumes) else None
-    if agg == _lib.MVN_AGG_CONF and vol_confidences is None:
-        raise TypeError("volume_aggregation_method '{}' needs vol_confidences".format(volume_aggregation_method))
-    feat = heatmaps.contiguous()
-    if feat.dtype not in (torch.float32, torch.bfloat16):
-        feat = feat.float()
-    proj = proj_matricies.float().contiguous()
-    conf = vol_confidences.float().contiguous() if agg == _lib.MVN_AGG_CONF else None
-    if proj.shape[:2] != feat.shape[:2] or proj.shape[2:] != (3, 4):
-        raise RuntimeError(f"proj_matricies shape {tuple(proj.shape)} does not match heatmaps {tuple(feat.shape)}")
-    if conf is not None and conf.shape != feat.shape[:3]:
-        raise RuntimeError(f"vol_confidences must be {tuple(feat.shape[:3])}, got {tuple(conf.shape)}")
+    feat, proj, conf = unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, volume_aggregation_method, cub)
     od = _dtype_code(out_dtype if out_dtype is not None else feat.dtype)
     if cub is not None:
-        if cub.batch != feat.shape[0]:
-            raise RuntimeError(f"cuboids for {cub.batch} frames, heatmaps have {feat.shape[0]}")
         if feat.shape[1] > 8:
             # in-kernel coordinates need the tiled kernel (N <= 8): materialise the volume
             coord_volumes, cub = cub.coord_volumes(), None

@@ -15,7 +15,7 @@ from torch import nn
 
 from . import _lib
 from ._ops import _require_gpu, _stream
-from .op import aggregation_code
+from .op import _dtype_code, aggregation_code, unproject_inputs
 
 CIN, COUT, KS = 32, 16, 7
 
@@ -51,9 +51,10 @@ def v2v_front(vol_cl, packed, scale, shift, out_dtype=torch.float32):
         raise RuntimeError("v2v_front needs a cubic volume")
     x = vol_cl.contiguous()
     _require_gpu(x, packed, scale, shift)
+    od = _dtype_code(out_dtype)
     out = torch.empty((B, COUT, V, V, V), dtype=out_dtype, device=x.device)
     code = _lib.load().mvn_v2v_front(x.data_ptr(), packed.data_ptr(), scale.data_ptr(), shift.data_ptr(),
-                                     out.data_ptr(), 0 if out_dtype == torch.float32 else 1, B, V, _stream(x))
+                                     out.data_ptr(), od, B, V, _stream(x))
     _lib.check(code, "mvn_v2v_front")
     return out
 
@@ -62,16 +63,15 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
                             out_dtype=torch.bfloat16, align_corners=False):
     """unproject_heatmaps (op.py:99-163) written channels-last: (B, Vx, Vy, Vz, C).
     ``coord_volumes`` may be a ``volumetric.Cuboids`` (coordinates formed in-kernel)."""
+    from .volumetric import Cuboids
     agg = aggregation_code(volume_aggregation_method)
     if agg == _lib.MVN_AGG_CONF:
         raise ValueError("unproject_channels_last: 'conf*' aggregation is not supported here")
-    feat = heatmaps.contiguous()
-    proj = proj_matricies.float().contiguous()
-    fd = 0 if feat.dtype == torch.float32 else 1
-    od = 0 if out_dtype == torch.float32 else 1
+    cub = coord_volumes if isinstance(coord_volumes, Cuboids) else None
+    feat, proj, _ = unproject_inputs(heatmaps, proj_matricies, None, agg, volume_aggregation_method, cub)
+    fd, od = _dtype_code(feat.dtype), _dtype_code(out_dtype)
     B, N, C, H, W = feat.shape
-    from .volumetric import Cuboids
-    if isinstance(coord_volumes, Cuboids) and N <= 8:
+    if cub is not None and N <= 8:
         # coordinates formed in-kernel from the per-frame cuboids (bit-identical, DESIGN.md 4.5)
         cub = coord_volumes
         _require_gpu(feat, proj, cub.params)
@@ -85,6 +85,8 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
     if isinstance(coord_volumes, Cuboids):
         coord_volumes = coord_volumes.coord_volumes()
     coords = coord_volumes.float().contiguous()
+    if coords.dim() != 5 or coords.shape[0] != B or coords.shape[4] != 3:
+        raise RuntimeError(f"coord_volumes must be ({B}, Vx, Vy, Vz, 3), got {tuple(coords.shape)}")
     _require_gpu(feat, proj, coords)
     Vx, Vy, Vz = coords.shape[1:4]
     out = torch.empty((B, Vx, Vy, Vz, C), dtype=out_dtype, device=feat.device)

@@ -97,13 +97,13 @@ def coord_volumes(base_points, cuboid_side, volume_size, thetas, kind="coco", tr
 
 
 def nearest_voxel(coords, keypoints):
-    """(B,Vx,Vy,Vz,3), (B,J,3) -> (B,J) flat index of the nearest voxel: argmin of the f32
-    squared distance summed x, y, z in order (loss.py:63), first index on ties — the
-    kernel's rule (csrc/ce_loss.hip)."""
+    """(B,Vx,Vy,Vz,3), (B,J,3) -> (B,J) flat index of the nearest voxel (loss.py:63-66):
+    f32 squared distance summed x, y, z in order, its IEEE square root, argmin with the
+    first index on ties (distinct squared distances can round to one root)."""
     f = np.float32
     c = np.asarray(coords, f).reshape(len(coords), -1, 3)
     k = np.asarray(keypoints, f)
     d = c[:, None, :, :] - k[:, :, None, :]
     sq = (d * d).astype(f)
     d2 = ((sq[..., 0] + sq[..., 1]).astype(f) + sq[..., 2]).astype(f)
-    return d2.argmin(axis=2)
+    return np.sqrt(d2).argmin(axis=2)

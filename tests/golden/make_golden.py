@@ -2,7 +2,7 @@
 
 Run in the build container only (it needs /root/reference; the GPU box never runs it):
 
-    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes|ce_loss|v2v_front]   (argument: only that fixture)
+    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes|ce_loss|v2v_front|chains]   (argument: only that fixture)
 
 The reference (learnable-triangulation-pytorch, mvn/utils/op.py and
 mvn/utils/multiview.py) is imported read-only with two in-memory accommodations:
@@ -200,6 +200,124 @@ def golden_v2v_front():
          bn_var=bn.running_var.numpy(), eps=np.float64(bn.eps), y=y.numpy())
 
 
+class _Cfg(dict):
+    """dict with attribute access (the reference's configs are EasyDicts; easydict is absent)."""
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError:
+            raise AttributeError(k) from None
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+def _cfg(d):
+    return _Cfg({k: _cfg(v) if isinstance(v, dict) else v for k, v in d.items()})
+
+
+class _FixedBackbone(torch.nn.Module):
+    """Stands in for PoseResNet: returns fixed (heatmaps, features, alg_conf, vol_conf)."""
+
+    def __init__(self, outs):
+        super().__init__()
+        self.outs = outs
+
+    def forward(self, images):
+        return self.outs
+
+
+class _ChannelSlice(torch.nn.Module):
+    """Stands in for V2VModel(32, 17): channels [0:17] of the unprojected volume (the bench's
+    V2V stand-in); keeps its input so the unprojection is pinned too."""
+
+    def forward(self, v):
+        self.last_input = v.detach().clone()
+        return v[:, :17]
+
+
+def golden_chains():
+    """End-to-end caller chains of the two models (last row), run through the
+    reference's own forward() with the backbone replaced by fixed outputs:
+      * AlgebraicTriangulationNet.forward (triangulation.py:149-200): integrate_tensor_2d of
+        heatmaps * 100 -> confidence normalisation -> upscale to image px -> DLT; also a
+        float64 re-run of the same forward (solver precision only);
+      * VolumetricTriangulationNet.forward (triangulation.py:245-355), training mode (random
+        cuboid rotation, seeded), kind 'mpii', softmax aggregation: camera resize ->
+        projections, coordinate volumes, process_features (a 1x1 conv set to pass channels
+        0..31 through exactly), unproject, V2V replaced by the channel slice [0:17],
+        soft-argmax with volume_multiplier."""
+    from copy import deepcopy
+    from mvn.models.triangulation import AlgebraicTriangulationNet, VolumetricTriangulationNet  # noqa: WPS433
+    from mvn.utils.multiview import Camera  # noqa: WPS433
+    bb = dict(name="resnet18", style="simple", init_weights=False, checkpoint="", num_joints=17, num_layers=18)
+    B, N, J = 2, 4, 17
+    out = {}
+
+    # --- algebraic: blob heatmaps at the projected joints (+ noise), GAP-head confidences
+    ab = synth.algebraic_batch(B, N, J, seed=40, noise_px=0.0)
+    rng = np.random.default_rng(40)
+    Hm = 96
+    uv = ab.points.numpy() / (384 / Hm) + rng.normal(0, 0.7, (B, N, J, 2))
+    yy, xx = np.mgrid[0:Hm, 0:Hm]
+    d2 = (xx - uv[..., 0, None, None]) ** 2 + (yy - uv[..., 1, None, None]) ** 2
+    # float16-representable values (stored as float16: the fixture stays small, exact in f32)
+    hm = (np.exp(-d2 / (2 * 2.0 ** 2)) + 0.02 * rng.standard_normal(d2.shape)).astype(np.float16).astype(np.float32)
+    conf = rng.uniform(0.2, 1.0, (B * N, J)).astype(np.float32)
+    cfg = _cfg(dict(model=dict(use_confidences=True, heatmap_softmax=True, heatmap_multiplier=100.0, backbone=bb)))
+    net = AlgebraicTriangulationNet(cfg, device="cpu").eval()
+    images = torch.zeros((B, N, 3, 384, 384))
+    for prec, dt in (("", torch.float32), ("64", torch.float64)):
+        net.backbone = _FixedBackbone((torch.from_numpy(hm).reshape(B * N, J, Hm, Hm).to(dt), None,
+                                       torch.from_numpy(conf).to(dt), None))
+        with torch.no_grad():
+            kp3, kp2, _, confn = net(images, ab.proj.to(dt), None)
+        out[f"alg_kp3d{prec}"] = kp3.numpy()
+        out[f"alg_kp2d{prec}"] = kp2.numpy()
+        out[f"alg_conf_norm{prec}"] = confn.numpy()
+    out.update(alg_heatmaps=hm.reshape(B, N, J, Hm, Hm).astype(np.float16), alg_conf=conf.reshape(B, N, J), alg_proj=ab.proj.numpy(),
+               alg_multiplier=np.float32(100.0))
+
+    # --- volumetric
+    V, Hv, side = 32, 32, 2500.0
+    cfg = _cfg(dict(model=dict(kind="mpii", volume_aggregation_method="softmax", volume_softmax=True,
+                               volume_multiplier=1.0, volume_size=V, cuboid_side=side, use_gt_pelvis=False,
+                               heatmap_softmax=True, heatmap_multiplier=100.0, backbone=bb)))
+    net = VolumetricTriangulationNet(cfg, device="cpu")
+    net.train()                     # random cuboid rotation (triangulation.py:318-321), seeded below
+    with torch.no_grad():
+        w = torch.zeros_like(net.process_features[0].weight)
+        w[torch.arange(32), torch.arange(32)] = 1.0            # pass channels 0..31 through
+        net.process_features[0].weight.copy_(w)
+        net.process_features[0].bias.zero_()
+    net.volume_net = _ChannelSlice()
+    feat32 = rng.standard_normal((B, N, 32, Hv, Hv)).astype(np.float32)
+    feats = np.zeros((B * N, 256, Hv, Hv), np.float32)
+    feats[:, :32] = feat32.reshape(B * N, 32, Hv, Hv)
+    net.backbone = _FixedBackbone((torch.zeros((B * N, J, Hv, Hv)), torch.from_numpy(feats), None, None))
+    cams = [[None] * B for _ in range(N)]
+    for b in range(B):
+        for v, c in enumerate(synth.ring_cameras(N, np.random.default_rng([41, b]))):
+            cams[v][b] = Camera(c.R, c.t, c.K)
+    pred = (np.array([0.0, 0.0, 900.0]) + rng.uniform(-300, 300, (B, J, 3)))
+    batch = {"cameras": cams, "pred_keypoints_3d": pred}
+    np.random.seed(42)
+    thetas = np.array([np.random.uniform(0.0, 2 * np.pi) for _ in range(B)])
+    np.random.seed(42)
+    with torch.no_grad():
+        kp3, _, vols, _, _, cv, base = net(torch.zeros((B, N, 3, 384, 384)), None, batch)
+    new = deepcopy(cams)
+    for v in range(N):
+        for b in range(B):
+            new[v][b].update_after_resize((384, 384), (Hv, Hv))
+    P = np.stack([np.stack([new[v][b].projection for v in range(N)]) for b in range(B)]).astype(np.float32)
+    sub = (slice(None), slice(None), slice(None, None, 4), slice(None, None, 4), slice(None, None, 4))
+    out.update(vol_features=feat32, vol_proj=P, vol_base=pred[:, 6], vol_thetas=thetas, vol_side=np.float64(side),
+               vol_coords=cv.numpy(), vol_kp3d=kp3.numpy(), vol_volumes_sub=vols.numpy()[sub],
+               vol_unprojected_sub=net.volume_net.last_input.numpy()[sub], vol_base_points=base.numpy())
+    save("chains.npz", **out)
+
+
 def main():
     op, multiview = import_reference()
     if len(sys.argv) > 1 and sys.argv[1] == "v2v_front":
@@ -213,6 +331,9 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "coord_volumes":
         golden_coord_volumes()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "chains":
+        golden_chains()
         return
     torch.manual_seed(0)
 
@@ -310,6 +431,7 @@ def main():
     golden_coord_volumes()
     golden_ce_loss()
     golden_v2v_front()
+    golden_chains()
 
 
 if __name__ == "__main__":

@@ -36,7 +36,7 @@ def test_unproject_backward_matches_reference_autograd(golden, device, method, a
 
 
 @pytest.mark.parametrize("method", ("sum", "softmax"))
-def test_unproject_backward_lds_overflow_path(golden, device, monkeypatch, method):
+def test_unproject_backward_lds_overflow_path(golden, device, method):
     """Blocks whose footprint exceeds the backward LDS budget scatter with global atomics."""
     from mvn_rocm import op, synth
     vb = synth.volumetric_batch(2, n_views=4, channels=6, heatmap=96, volume=16, seed=3)

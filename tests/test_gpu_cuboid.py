@@ -56,22 +56,20 @@ def test_unproject_cuboid_is_bit_identical_to_the_volume_path(device, n_views, m
             np.testing.assert_array_equal(a.cpu().numpy(), ref)
 
 
-def test_unproject_cuboid_bf16_and_every_kernel_path(device, monkeypatch):
+def test_unproject_cuboid_bf16_and_every_kernel_path(device):
     from mvn_rocm import op, synth
     B, V = 2, 24
     vb = synth.volumetric_batch(B, n_views=4, channels=8, volume=8, seed=5)
     cub, _ = _frames(B, V, seed=9)
     coords = cub.coord_volumes()
     feat, proj = vb.features.to(device).to(torch.bfloat16), vb.proj.to(device)
-    for budget in (None, "300", "40"):        # one pass, several passes, global-gather fallback
-        if budget is None:
-            monkeypatch.delenv("MVN_UNPROJECT_LDS_SLOTS", raising=False)
-        else:
-            monkeypatch.setenv("MVN_UNPROJECT_LDS_SLOTS", budget)
-        for od in (None, torch.float32):
-            a = op.unproject_heatmaps(feat, proj, cub, "softmax", out_dtype=od)
-            b = op.unproject_heatmaps(feat, proj, coords, "softmax", out_dtype=od)
-            assert torch.equal(_bits(a), _bits(b)), budget
+    from mvn_rocm import _lib
+    for budget in (0, 300, 40):        # one pass, several passes, global-gather fallback
+        with _lib.unproject_knobs(budget):
+            for od in (None, torch.float32):
+                a = op.unproject_heatmaps(feat, proj, cub, "softmax", out_dtype=od)
+                b = op.unproject_heatmaps(feat, proj, coords, "softmax", out_dtype=od)
+                assert torch.equal(_bits(a), _bits(b)), budget
 
 
 def test_unproject_cuboid_more_than_8_views_materialises(device):
@@ -133,15 +131,23 @@ def test_cuboid_gradients_match_the_volume_path(device):
     assert max_rel(grads[0].cpu().numpy(), grads[1].cpu().numpy()) <= 1e-5
 
 
+@pytest.mark.parametrize("n_views", (4, 8))
 @pytest.mark.parametrize("dt", (torch.float32, torch.bfloat16))
-def test_channels_last_cuboid_is_bit_identical(device, dt):
-    """Config 5's channels-last unprojection (V2V front input) with in-kernel coordinates."""
-    from mvn_rocm import synth, v2v
+def test_channels_last_cuboid_is_bit_identical(device, dt, n_views):
+    """Config 5's channels-last unprojection (V2V front input) with in-kernel coordinates:
+    bit-identical to the coordinate-volume path and a transpose of the NCDHW output, for
+    the 4- and 8-view instantiations (8 views: 2-channel packed stores) and on every
+    staging path (one LDS pass, several passes, global-gather fallback)."""
+    from mvn_rocm import _lib, op, synth, v2v
     B, V = 2, 32
-    vb = synth.volumetric_batch(B, n_views=4, channels=32, volume=8, seed=8)
+    vb = synth.volumetric_batch(B, n_views=n_views, channels=32, volume=8, seed=8)
     cub, _ = _frames(B, V, seed=8)
     feat, proj = vb.features.to(device).to(dt), vb.proj.to(device)
-    for od in ((torch.bfloat16, torch.float32) if dt == torch.bfloat16 else (torch.float32,)):
-        a = v2v.unproject_channels_last(feat, proj, cub, "softmax", out_dtype=od)
-        b = v2v.unproject_channels_last(feat, proj, cub.coord_volumes(), "softmax", out_dtype=od)
-        assert a.shape == (B, V, V, V, 32) and torch.equal(_bits(a), _bits(b))
+    for budget in (0, 300, 40):
+        with _lib.unproject_knobs(budget):
+            for od in ((torch.bfloat16, torch.float32) if dt == torch.bfloat16 else (torch.float32,)):
+                a = v2v.unproject_channels_last(feat, proj, cub, "softmax", out_dtype=od)
+                b = v2v.unproject_channels_last(feat, proj, cub.coord_volumes(), "softmax", out_dtype=od)
+                assert a.shape == (B, V, V, V, 32) and torch.equal(_bits(a), _bits(b)), budget
+                c = op.unproject_heatmaps(feat, proj, cub, "softmax", out_dtype=od)
+                assert torch.equal(_bits(a), _bits(c.permute(0, 2, 3, 4, 1).contiguous())), budget

@@ -82,7 +82,7 @@ def tile_footprints(proj, coords, H, W, tile):
 @pytest.mark.parametrize("n_views", (4, 8))
 @pytest.mark.parametrize("path", ("lds_1pass", "lds_multipass", "global_fallback", "simple"))
 @pytest.mark.parametrize("method", METHODS)
-def test_unproject_every_kernel_path(device, monkeypatch, path, method, n_views):
+def test_unproject_every_kernel_path(device, path, method, n_views):
     """Each code path of the unprojection — one LDS pass, several LDS passes, the
     global-gather fallback and the simple kernel — against the oracle, for the 4- and
     8-view instantiations."""
@@ -90,20 +90,19 @@ def test_unproject_every_kernel_path(device, monkeypatch, path, method, n_views)
     vb = synth.volumetric_batch(2, n_views=n_views, channels=10, heatmap=64, volume=32, seed=31)
     feat, proj, coords = vb.features.numpy(), vb.proj.numpy(), vb.coords.numpy()
     areas = tile_footprints(proj, coords, 64, 64, (4, 8, 16))     # TileShape<4>, <8> in unproject_tiled.hip
+    budget, simple = 0, path == "simple"
     if path == "lds_multipass":        # every footprint fits alone, no tile's views fit together
         budget = int(areas.max()) + 64        # margin: the kernel rounds in f32
         assert (areas.sum(1) + 1 > budget).any()
-        monkeypatch.setenv("MVN_UNPROJECT_LDS_SLOTS", str(budget))
     elif path == "global_fallback":    # some single footprints exceed the budget
         budget = int(np.median(areas[areas > 0]))
         assert (areas.max(1) > budget - 1).any() and (areas.max(1) <= budget - 1).any()
-        monkeypatch.setenv("MVN_UNPROJECT_LDS_SLOTS", str(budget))
-    elif path == "simple":
-        monkeypatch.setenv("MVN_UNPROJECT_KERNEL", "simple")
     conf = np.random.default_rng(2).uniform(0, 1, (2, n_views, 10)).astype(np.float32)
     ref = capi.unproject(feat, proj, coords, method, conf)
-    out = _op().unproject_heatmaps(vb.features.to(device), vb.proj.to(device), vb.coords.to(device), method,
-                                   _t(conf, device))
+    from mvn_rocm import _lib
+    with _lib.unproject_knobs(budget, simple):
+        out = _op().unproject_heatmaps(vb.features.to(device), vb.proj.to(device), vb.coords.to(device), method,
+                                       _t(conf, device))
     assert_unproject_parity(out.cpu().numpy(), ref, method)
 
 

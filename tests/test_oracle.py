@@ -201,3 +201,33 @@ def test_v2v_front_folding_and_packing(golden):
     w = t["weight"].reshape(16, 32, 343)
     for tap, lane, j in ((0, 0, 0), (123, 37, 5), (342, 63, 7), (200, 16, 0)):
         assert float(packed[tap, lane, j]) == float(w[lane % 16, 8 * (lane // 16) + j, tap].bfloat16())
+
+
+# ----------------------------------------------------------------------------- caller chains
+def test_chain_golden_pins_the_oracles(golden):
+    """tests/golden/chains.npz ran the reference models' own forward() (triangulation.py:149-200,
+    :245-355) with fixed backbone outputs.  The oracles reproduce every stage of it: the
+    coordinate volumes (numpy recipe, bit-exact), the unprojection (C restatement,
+    bit-exact for the f32 path up to the softmax exp), the soft-argmax and the DLT."""
+    d = golden("chains.npz")
+    # volumetric: coordinate volumes, unprojection, soft-argmax (multiplier 1.0, softmax)
+    cv = restate_np.coord_volumes(d["vol_base"], float(d["vol_side"]), 32, d["vol_thetas"], "mpii", False)
+    np.testing.assert_array_equal(cv, d["vol_coords"])
+    np.testing.assert_array_equal(d["vol_base_points"], d["vol_base"].astype(np.float32))
+    vol = capi.unproject(d["vol_features"], d["vol_proj"], cv, "softmax")
+    sub = (slice(None), slice(None), slice(None, None, 4), slice(None, None, 4), slice(None, None, 4))
+    assert max_rel(vol[sub], d["vol_unprojected_sub"]) <= 1e-6
+    xyz, sm = capi.softargmax3d(vol[:, :17], cv, True, 1.0)
+    assert max_rel(xyz, d["vol_kp3d"]) <= 1e-5
+    assert max_rel(sm[sub], d["vol_volumes_sub"]) <= 1e-5
+    # algebraic: 2D soft-argmax of heatmaps * 100, confidence normalisation, upscale, DLT
+    B, N, J, H, W = d["alg_heatmaps"].shape
+    hm = d["alg_heatmaps"].astype(np.float32).reshape(B * N, J, H, W) * d["alg_multiplier"]
+    xy, _ = restate_np.integrate_tensor_2d(hm, True)
+    kp2 = xy.reshape(B, N, J, 2) * np.array([384 / W, 384 / H])
+    assert max_rel(kp2, d["alg_kp2d64"]) <= 1e-6
+    conf = d["alg_conf"].astype(np.float64)
+    conf = conf / conf.sum(1, keepdims=True) + 1e-5
+    x64 = restate_np.triangulate_batch_of_points(d["alg_proj"], kp2, conf)
+    assert max_rel(x64, d["alg_kp3d64"]) <= 1e-6
+    assert max_rel(d["alg_kp3d"], d["alg_kp3d64"]) <= 1e-3     # the f32 reference's own SVD error

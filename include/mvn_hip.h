@@ -259,7 +259,8 @@ int mvn_dlt_backward(const float* proj, const float* pts, const float* conf, con
  * Test hook (tests only; process-wide, thread-safe): force unprojection code paths.
  *   lds_slots  > 0: LDS slot budget per staging pass of the tiled kernel (small budgets
  *              force the multi-pass and global-gather paths); 0 = the kernel's own budget
- *   kernel     0 = default dispatch, 1 = the simple register-geometry kernel
+ *   kernel     0 = default dispatch, 1 = the simple register-geometry kernel,
+ *              2 = the generic tiled kernel (skip the four-view kernel)
  * Returns MVN_OK, or MVN_ERR_ARG for a negative budget or an unknown kernel.
  */
 int mvn_debug_set_unproject(int lds_slots, int kernel);

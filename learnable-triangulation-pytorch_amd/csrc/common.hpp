@@ -79,6 +79,7 @@ inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
 // kernel paths; nothing is read from the environment on the launch path.
 int unproject_lds_slot_budget();   // 0 = the kernel's own budget
 bool unproject_force_simple();
+bool unproject_force_generic();    // skip the four-view kernel (unproject_x4.hip)
 
 // XCD-aware block order (cdna_hip_programming.md §5.5 T1, bijective form): hardware deals
 // blocks round-robin over the 8 XCDs, so block b runs on XCD b % 8.  Remapping gives each

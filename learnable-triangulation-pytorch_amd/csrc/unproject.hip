@@ -72,15 +72,16 @@ __global__ __launch_bounds__(kUnprojBlock) void unproject_regviews(
       float m = s[0];
 #pragma unroll
       for (int v = 1; v < kMaxRegViews; ++v) if (v < N) m = fmaxf(m, s[v]);
+      const float ml = m * kLog2e;
       float den = 0.f, num = 0.f;
 #pragma unroll
       for (int v = 0; v < kMaxRegViews; ++v)
         if (v < N) {
-          const float e = __expf(s[v] - m);
+          const float e = softmax_exp(s[v], ml);
           den += e;
           num = __builtin_fmaf(s[v], e, num);
         }
-      r = num / den;
+      r = num * __builtin_amdgcn_rcpf(den);
     }
     store_elem(ob + size_t(c) * nvox, r);
   }
@@ -212,11 +213,12 @@ namespace {
 std::atomic<int> g_lds_slots{0}, g_force_simple{0};
 }  // namespace
 int unproject_lds_slot_budget() { return g_lds_slots.load(std::memory_order_relaxed); }
-bool unproject_force_simple() { return g_force_simple.load(std::memory_order_relaxed) != 0; }
+bool unproject_force_simple() { return g_force_simple.load(std::memory_order_relaxed) == 1; }
+bool unproject_force_generic() { return g_force_simple.load(std::memory_order_relaxed) == 2; }
 }  // namespace mvn
 
 extern "C" int mvn_debug_set_unproject(int lds_slots, int kernel) {
-  if (lds_slots < 0 || (kernel != 0 && kernel != 1)) return MVN_ERR_ARG;
+  if (lds_slots < 0 || kernel < 0 || kernel > 2) return MVN_ERR_ARG;
   mvn::g_lds_slots.store(lds_slots, std::memory_order_relaxed);
   mvn::g_force_simple.store(kernel, std::memory_order_relaxed);
   return MVN_OK;

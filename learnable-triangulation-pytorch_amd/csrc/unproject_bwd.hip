@@ -136,8 +136,8 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
 #pragma unroll
         for (int v = 1; v < NV; ++v) if (v < N) m = fmaxf(m, s[v]);
 #pragma unroll
-        for (int v = 0; v < NV; ++v) if (v < N) { const float e = __expf(s[v] - m); den += e; out = __builtin_fmaf(s[v], e, out); }
-        out /= den;
+        for (int v = 0; v < NV; ++v) if (v < N) { const float e = softmax_exp(s[v], m * kLog2e); den += e; out = __builtin_fmaf(s[v], e, out); }
+        out *= __builtin_amdgcn_rcpf(den);
       }
       if constexpr (AGG == MVN_AGG_MAX) {
 #pragma unroll
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
         if constexpr (AGG == MVN_AGG_SUM) coef[v] = g;
         else if constexpr (AGG == MVN_AGG_CONF) coef[v] = g * conf[(size_t(b) * N + v) * C + c];
         else if constexpr (AGG == MVN_AGG_MAX) coef[v] = v == arg ? g : 0.f;
-        else coef[v] = g * (__expf(s[v] - m) / den) * (1.f + s[v] - out);
+        else coef[v] = g * (softmax_exp(s[v], m * kLog2e) * __builtin_amdgcn_rcpf(den)) * (1.f + s[v] - out);
         if (coef[v] != 0.f) {
           float* pl = gfb + (size_t(v) * C + c) * HW;
           if (tp[v].w0 != 0.f) atomicAdd(pl + tp[v].o0, coef[v] * tp[v].w0);
@@ -232,8 +232,8 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
         for (int v = 1; v < NV; ++v) if (v < N) m = fmaxf(m, s[v][k]);
         float den = 0.f, out = 0.f, e[NV];
 #pragma unroll
-        for (int v = 0; v < NV; ++v) { e[v] = v < N ? __expf(s[v][k] - m) : 0.f; den += e[v]; out = __builtin_fmaf(s[v][k], e[v], out); }
-        const float inv = 1.f / den;
+        for (int v = 0; v < NV; ++v) { e[v] = v < N ? softmax_exp(s[v][k], m * kLog2e) : 0.f; den += e[v]; out = __builtin_fmaf(s[v][k], e[v], out); }
+        const float inv = __builtin_amdgcn_rcpf(den);
         out *= inv;
 #pragma unroll
         for (int v = 0; v < NV; ++v) coef[v] = g[k] * e[v] * inv * (1.f + s[v][k] - out);

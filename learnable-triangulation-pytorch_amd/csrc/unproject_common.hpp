@@ -1,10 +1,23 @@
 // Shared device code of the unprojection kernels (unproject.hip, unproject_tiled.hip).
 #pragma once
 
+#include <climits>
+
 #include "common.hpp"
 
 namespace mvn {
 namespace unproj {
+
+// ---- the one f32 form of the cross-view softmax (op.py:153-159) ----------------------
+// Every unprojection path — the staged LDS paths, the global-gather fallback, the simple
+// kernels and the backward — evaluates it the same way, so a tensor never mixes two
+// roundings (which path a tile takes depends on LDS budget and camera distance):
+//   m = max_v s_v;  e_v = exp2(fma(s_v, log2 e, -(m * log2 e)));  den = ((e_0 + e_1) + ...);
+//   value = fma chain of s_v * e_v, times rcp(den).   (<= 1e-5 of the reference's softmax)
+constexpr float kLog2e = 1.4426950408889634f;
+__device__ __forceinline__ float softmax_exp(float s, float ml) {   // ml = m * kLog2e
+  return __builtin_amdgcn_exp2f(__builtin_fmaf(s, kLog2e, -ml));
+}
 
 // Bilinear taps of one voxel in one view: 4 clamped plane offsets + 4 weights.
 // Out-of-bounds corners and invalid (behind-camera) voxels get weight 0, which is
@@ -165,17 +178,86 @@ __device__ __forceinline__ float aggregate(const float (&s)[NV], int N, const fl
     float m = s[0];
 #pragma unroll
     for (int v = 1; v < NV; ++v) if (v < N) m = fmaxf(m, s[v]);
+    const float ml = m * kLog2e;
     float den = 0.f, num = 0.f;
 #pragma unroll
     for (int v = 0; v < NV; ++v)
       if (v < N) {
-        const float e = __expf(s[v] - m);
+        const float e = softmax_exp(s[v], ml);
         den += e;
         num = __builtin_fmaf(s[v], e, num);
       }
-    r = num / den;
+    r = num * __builtin_amdgcn_rcpf(den);
   }
   return r;
+}
+
+constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any frame
+
+// Wave-wide integer min / max, returned wave-uniform.  row_shr DPP steps (identity
+// shifted in) leave each row's reduction in its lane 15; four readlanes combine the rows.
+__device__ __forceinline__ int wave_min_u(int v) {
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xf, 0xf, false));
+  return min(min(__builtin_amdgcn_readlane(v, 15), __builtin_amdgcn_readlane(v, 31)),
+             min(__builtin_amdgcn_readlane(v, 47), __builtin_amdgcn_readlane(v, 63)));
+}
+__device__ __forceinline__ int wave_max_u(int v) {
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));
+  return max(max(__builtin_amdgcn_readlane(v, 15), __builtin_amdgcn_readlane(v, 31)),
+             max(__builtin_amdgcn_readlane(v, 47), __builtin_amdgcn_readlane(v, 63)));
+}
+
+// Buffer descriptor from block-uniform inputs, provably in SGPRs (cdna_hip_programming.md T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(a >> 32));
+  void* p = reinterpret_cast<void*>((uint64_t(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, int(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
+}
+
+// One voxel, all channels, taps gathered from global memory (oversize-footprint fallback).
+// Rolled loops and geometry recomputed per (channel, view): slow but register-lean, so
+// the staged path's register allocation is unaffected.  Same arithmetic and op order.
+template <int AGG, typename TIn, typename TOut>
+__device__ __forceinline__ void gather_voxel(const TIn* __restrict__ fb, const float* __restrict__ Pb,
+                                             const float* __restrict__ cfb, TOut* __restrict__ ov, int nvox,
+                                             int N, int C, int H, int W, float x, float y, float z,
+                                             int align_corners) {
+  const size_t HW = size_t(H) * W;
+#pragma unroll 1
+  for (int c = 0; c < C; ++c) {
+    float r = 0.f, m = 0.f, den = 0.f;
+#pragma unroll 1
+    for (int pass = 0; pass < (AGG == MVN_AGG_SOFTMAX ? 2 : 1); ++pass) {
+#pragma unroll 1
+      for (int v = 0; v < N; ++v) {
+        const float sv = sample(fb + (size_t(v) * C + c) * HW, view_taps(Pb + v * 12, x, y, z, H, W, align_corners));
+        if constexpr (AGG == MVN_AGG_SUM) {
+          r = v == 0 ? sv : r + sv;
+        } else if constexpr (AGG == MVN_AGG_MAX) {
+          r = (v == 0 || sv > r) ? sv : r;
+        } else if constexpr (AGG == MVN_AGG_CONF) {
+          const float p = sv * cfb[size_t(v) * C + c];
+          r = v == 0 ? p : r + p;
+        } else if (pass == 0) {
+          m = v == 0 ? sv : fmaxf(m, sv);
+        } else {
+          const float e = softmax_exp(sv, m * kLog2e);
+          den += e;
+          r = __builtin_fmaf(sv, e, r);
+        }
+      }
+    }
+    if constexpr (AGG == MVN_AGG_SOFTMAX) r = r * __builtin_amdgcn_rcpf(den);
+    store_elem(ov + size_t(c) * nvox, r);
+  }
 }
 
 // Launchers (defined in unproject_tiled.hip); return MVN_OK or an error code.
@@ -185,6 +267,121 @@ template <int AGG, typename TIn, typename TOut>
 int launch_tiled(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
                  const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
                  int align_corners, int out_cl, hipStream_t s);
+
+// ---- helpers of the four-view kernels (unproject_x4.hip, unproject_w4.hip) ------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <typename TIn> struct ChunkT;               // 4 pixels of one channel plane
+template <> struct ChunkT<float> { using type = uint4; };
+template <> struct ChunkT<uint16_t> { using type = uint2; };
+
+template <typename TIn>
+__device__ __forceinline__ typename ChunkT<TIn>::type load_chunk(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
+template <>
+__device__ __forceinline__ uint4 load_chunk<float>(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+  const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, v, s, 0);
+  return make_uint4(q[0], q[1], q[2], q[3]);
+}
+template <>
+__device__ __forceinline__ uint2 load_chunk<uint16_t>(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+  const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, v, s, 0);
+  return make_uint2(q[0], q[1]);
+}
+// f32 bits of pixel p (0..3) of a chunk
+__device__ __forceinline__ uint32_t chunk_px(const uint4& q, int p) {
+  return p == 0 ? q.x : p == 1 ? q.y : p == 2 ? q.z : q.w;
+}
+__device__ __forceinline__ uint32_t chunk_px(const uint2& q, int p) {
+  const uint32_t d = p < 2 ? q.x : q.y;
+  return (p & 1) ? (d & 0xffff0000u) : (d << 16);      // bf16 -> f32 bits, exact
+}
+
+__device__ __forceinline__ f2 lo2(const uint4& q) { return f2{__uint_as_float(q.x), __uint_as_float(q.y)}; }
+__device__ __forceinline__ f2 hi2(const uint4& q) { return f2{__uint_as_float(q.z), __uint_as_float(q.w)}; }
+
+// View aggregation of a channel pair (op.py:147-161), lane-wise the op order of
+// aggregate<> (sum / max / conf, reference order) and of aggregate_fast<> (softmax).
+template <int AGG>
+__device__ __forceinline__ f2 aggregate_pair(const f2 (&s)[4], const f2 (&cf)[4]) {
+  if constexpr (AGG == MVN_AGG_SUM) {
+    return ((s[0] + s[1]) + s[2]) + s[3];
+  } else if constexpr (AGG == MVN_AGG_MAX) {
+    f2 r = s[0];
+#pragma unroll
+    for (int v = 1; v < 4; ++v) {
+      r.x = s[v].x > r.x ? s[v].x : r.x;
+      r.y = s[v].y > r.y ? s[v].y : r.y;
+    }
+    return r;
+  } else if constexpr (AGG == MVN_AGG_CONF) {
+    f2 r = s[0] * cf[0];
+#pragma unroll
+    for (int v = 1; v < 4; ++v) r = r + s[v] * cf[v];
+    return r;
+  } else {
+    constexpr float kLog2e = 1.4426950408889634f;
+    f2 m;
+    m.x = fmaxf(fmaxf(fmaxf(s[0].x, s[1].x), s[2].x), s[3].x);
+    m.y = fmaxf(fmaxf(fmaxf(s[0].y, s[1].y), s[2].y), s[3].y);
+    const f2 nml = -(m * f2{kLog2e, kLog2e});
+    f2 e[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const f2 a = pk_fma(s[v], f2{kLog2e, kLog2e}, nml);
+      e[v] = f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+    }
+    // den = ((0 + e0) + e1 + ...), num = fma(s, e, num) from 0: e0 + 0 == e0 and
+    // fma(s0, e0, 0) == s0 * e0 exactly, so the first terms start the chains
+    const f2 den = ((e[0] + e[1]) + e[2]) + e[3];
+    const f2 num = pk_fma(s[3], e[3], pk_fma(s[2], e[2], pk_fma(s[1], e[1], s[0] * e[0])));
+    return num * f2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  }
+}
+
+template <typename T> __device__ __forceinline__ void store_plane(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
+template <> __device__ __forceinline__ void store_plane<float>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, 0);
+}
+template <> __device__ __forceinline__ void store_plane<uint16_t>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, 0);
+}
+
+// Per-view region of the LDS image (block-uniform, SGPRs).
+struct Region {
+  int x0, y0, bw, bh, pitch, sbase, xa, cw, cbase, pass, cend;
+  float inv_cw;
+};
+
+// rg[u] for a runtime u, field by field through selects (an indexed copy of the struct
+// array would go through scratch memory).
+// (each operand goes through readfirstlane — a no-op on these uniform values — so that the
+// select is not folded into an indexed load from a stack copy of the array.)
+__device__ __forceinline__ int rfl(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+__device__ __forceinline__ Region pick_region(const Region (&rg)[4], int u) {
+  Region r;
+#define MVN_PICK(f) r.f = u == 0 ? rfl(rg[0].f) : u == 1 ? rfl(rg[1].f) : u == 2 ? rfl(rg[2].f) : rfl(rg[3].f)
+  MVN_PICK(x0); MVN_PICK(y0); MVN_PICK(bw); MVN_PICK(bh); MVN_PICK(pitch); MVN_PICK(sbase); MVN_PICK(xa);
+  MVN_PICK(cw); MVN_PICK(cbase); MVN_PICK(pass); MVN_PICK(cend); MVN_PICK(inv_cw);
+#undef MVN_PICK
+  return r;
+}
+
+
+// The wave-autonomous four-view kernel (unproject_w4.hip), same contract as launch_x4.
+template <int AGG, typename TIn, typename TOut>
+int launch_w4(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
+              const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+              int align_corners, int out_cl, hipStream_t s);
+
+// The four-view kernel (unproject_x4.hip): MVN_OK, an error code, or 1 when it does not
+// apply to the call (then launch_tiled runs the generic kernel).
+template <int AGG, typename TIn, typename TOut>
+int launch_x4(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
+              const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+              int align_corners, int out_cl, hipStream_t s);
 
 }  // namespace unproj
 }  // namespace mvn

@@ -41,7 +41,6 @@ namespace {
 #define MVN_STAGE_UNCOND 0   // 1: stage every slot unconditionally for 4 views as well
 #endif
 
-constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any frame
 
 // Tile of voxels per block (z fastest: a wave's output stores are 16-voxel = 64-byte runs
 // of a channel plane) and 16-byte LDS pixel slots per staging buffer (two per block; the
@@ -63,34 +62,6 @@ template <> struct TileShape<8> {
   static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 4096, G = MVN_G_8VIEWS;
   static constexpr int WAVES = G == 2 ? 4 : 2;
 };
-
-// Wave-wide integer min / max, returned wave-uniform.  row_shr DPP steps (identity
-// shifted in) leave each row's reduction in its lane 15; four readlanes combine the rows.
-__device__ __forceinline__ int wave_min_u(int v) {
-  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xf, 0xf, false));
-  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xf, 0xf, false));
-  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xf, 0xf, false));
-  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xf, 0xf, false));
-  return min(min(__builtin_amdgcn_readlane(v, 15), __builtin_amdgcn_readlane(v, 31)),
-             min(__builtin_amdgcn_readlane(v, 47), __builtin_amdgcn_readlane(v, 63)));
-}
-__device__ __forceinline__ int wave_max_u(int v) {
-  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));
-  return max(max(__builtin_amdgcn_readlane(v, 15), __builtin_amdgcn_readlane(v, 31)),
-             max(__builtin_amdgcn_readlane(v, 47), __builtin_amdgcn_readlane(v, 63)));
-}
-
-// Buffer descriptor from block-uniform inputs, provably in SGPRs (cdna_hip_programming.md T20).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(a >> 32));
-  void* p = reinterpret_cast<void*>((uint64_t(hi) << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(p, 0, int(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
-}
 
 template <typename T> __device__ __forceinline__ uint32_t buf_load(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
 template <> __device__ __forceinline__ uint32_t buf_load<float>(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
@@ -170,44 +141,6 @@ __device__ __forceinline__ SlotRegion find_region(int idx, int pass, int N, cons
   for (int u = 0; u < NV; ++u)
     if (u < N && rpass[u] == pass && idx >= rbase[u]) q = SlotRegion{u, rx[u], ry[u], rbw[u], rpitch[u], rbase[u], rinv[u]};
   return q;
-}
-
-// One voxel, all channels, taps gathered from global memory (oversize-footprint fallback).
-// Rolled loops and geometry recomputed per (channel, view): slow but register-lean, so
-// the staged path's register allocation is unaffected.  Same arithmetic and op order.
-template <int AGG, typename TIn, typename TOut>
-__device__ __forceinline__ void gather_voxel(const TIn* __restrict__ fb, const float* __restrict__ Pb,
-                                             const float* __restrict__ cfb, TOut* __restrict__ ov, int nvox,
-                                             int N, int C, int H, int W, float x, float y, float z,
-                                             int align_corners) {
-  const size_t HW = size_t(H) * W;
-#pragma unroll 1
-  for (int c = 0; c < C; ++c) {
-    float r = 0.f, m = 0.f, den = 0.f;
-#pragma unroll 1
-    for (int pass = 0; pass < (AGG == MVN_AGG_SOFTMAX ? 2 : 1); ++pass) {
-#pragma unroll 1
-      for (int v = 0; v < N; ++v) {
-        const float sv = sample(fb + (size_t(v) * C + c) * HW, view_taps(Pb + v * 12, x, y, z, H, W, align_corners));
-        if constexpr (AGG == MVN_AGG_SUM) {
-          r = v == 0 ? sv : r + sv;
-        } else if constexpr (AGG == MVN_AGG_MAX) {
-          r = (v == 0 || sv > r) ? sv : r;
-        } else if constexpr (AGG == MVN_AGG_CONF) {
-          const float p = sv * cfb[size_t(v) * C + c];
-          r = v == 0 ? p : r + p;
-        } else if (pass == 0) {
-          m = v == 0 ? sv : fmaxf(m, sv);
-        } else {
-          const float e = __expf(sv - m);
-          den += e;
-          r = __builtin_fmaf(sv, e, r);
-        }
-      }
-    }
-    if constexpr (AGG == MVN_AGG_SOFTMAX) r = r / den;
-    store_elem(ov + size_t(c) * nvox, r);
-  }
 }
 
 // NV = views held in registers (4 or 8); EXACT: the launch has exactly NV views, so every
@@ -540,6 +473,11 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
                  const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
                  int align_corners, int out_cl, hipStream_t s) {
   if (out_cl && C % 4 != 0) return MVN_ERR_SHAPE;
+  if (!unproject_force_generic()) {
+    const int r = launch_x4<AGG, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz,
+                                            align_corners, out_cl, s);
+    if (r != 1) return r;
+  }
   // 32-bit buffer offsets: a frame's maps and volume must stay below 2 GiB
   if ((long long)N * C * H * W * sizeof(TIn) >= (1LL << 31) ||
       (long long)C * Vx * Vy * Vz * sizeof(TOut) >= (1LL << 31))

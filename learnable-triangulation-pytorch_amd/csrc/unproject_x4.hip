@@ -1,0 +1,590 @@
+// Four-view unprojection for gfx950 — the production kernel behind mvn_unproject for the
+// configurations of BASELINE.json (4 views, W % 4 == 0, C % 4 == 0).
+//
+// Contract and numerics: mvn/utils/op.py:99-163 exactly as unproject_tiled.hip (sum / max /
+// conf bit-exact with the reference; softmax max-first with exp2 and one reciprocal, same
+// op order as unproject_tiled's staged path, so the two kernels agree bit for bit).
+//
+// What differs from unproject_tiled (the generic N <= 8 kernel) is how the per-block LDS
+// image of the views' footprints is filled and consumed:
+//   * staging in CHUNKS of 4 x-consecutive pixels: one 16-byte (f32) / 8-byte (bf16) buffer
+//     load per chunk and channel instead of one 4- / 2-byte load per pixel and channel —
+//     a quarter of the vector-memory instructions (the texture path, not HBM, was the
+//     busiest unit: TD 82 % at config 3, profiles/r07a_*).  Chunks start at x % 4 == 0, so
+//     with W % 4 == 0 a chunk lies wholly inside or wholly outside the image (the hardware
+//     range check of an out-of-range offset returns zeros = padding_mode 'zeros'); pixels
+//     of a chunk outside the block's footprint are simply not written to LDS.  The 4 x 4
+//     (pixel x channel) block a lane loads is transposed for free into 4 slots of
+//     (4 channels) 16 bytes, one ds_write_b128 each;
+//   * bilinear sampling and view aggregation on channel PAIRS with packed f32 arithmetic
+//     (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32: per lane exactly the scalar fma / mul /
+//     add of the reference order, two channels per instruction).
+// Everything else — voxel tile per block (TX x 8 x 16, z fastest), per-view footprint
+// bounding boxes with odd row pitch, two LDS buffers with the next channel group's loads
+// in flight, XCD-balanced block order, buffer-descriptor stores — follows unproject_tiled.
+// Footprints that exceed one LDS buffer are staged in several passes of whole views;
+// a single view larger than a buffer sends its block to the global-gather fallback.
+#include "unproject_common.hpp"
+
+// Ablation switches for A/B builds (tools/build_x4_variant.sh); all 0 in the library.
+#ifndef MVN_X4_ABL_NOSTORE
+#define MVN_X4_ABL_NOSTORE 0   // 1: outputs stored only if the value equals a sentinel (no traffic)
+#endif
+#ifndef MVN_X4_ABL_NOSTAGE
+#define MVN_X4_ABL_NOSTAGE 0   // 1: stage the first channel group only (later groups reuse it)
+#endif
+#ifndef MVN_X4_ABL_BCAST
+#define MVN_X4_ABL_BCAST 0     // 1: every lane reads its wave's first lane's taps (no bank conflicts)
+#endif
+
+#ifndef MVN_X4_STAMPS
+#define MVN_X4_STAMPS 0        // 1: diagnostic build, per-block phase timestamps (mvn_x4_stamps)
+#endif
+#if MVN_X4_STAMPS
+__device__ unsigned long long g_x4_stamps[1 << 21];
+#define X4_STAMP(i)                                                                            \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 21) / 16)                                      \
+      g_x4_stamps[blockIdx.x * 16 + (i)] = (i) == 0 ? __builtin_amdgcn_s_memrealtime()         \
+                                                    : __builtin_amdgcn_s_memtime();            \
+  } while (0)
+#define X4_ACC_DECL unsigned long long x4_acc[4] = {0, 0, 0, 0}, x4_t = __builtin_amdgcn_s_memtime()
+#define X4_ACC(k)                                                                              \
+  do {                                                                                         \
+    const unsigned long long x4_n = __builtin_amdgcn_s_memtime();                              \
+    x4_acc[k] += x4_n - x4_t;                                                                  \
+    x4_t = x4_n;                                                                               \
+  } while (0)
+#define X4_ACC_STORE                                                                           \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 21) / 16)                                      \
+      for (int k = 0; k < 4; ++k) g_x4_stamps[blockIdx.x * 16 + 8 + k] = x4_acc[k];           \
+  } while (0)
+#else
+#define X4_STAMP(i) do {} while (0)
+#define X4_ACC_DECL do {} while (0)
+#define X4_ACC(k) do {} while (0)
+#define X4_ACC_STORE do {} while (0)
+#endif
+
+#ifndef MVN_USE_W4
+#define MVN_USE_W4 0     // 1: four-view calls go to the wave-autonomous kernel (unproject_w4.hip)
+#endif
+#ifndef MVN_X4_TILE
+#define MVN_X4_TILE -1   // voxel tile: 0 = 4x8x16 (512 threads), 1 = 8x8x8 (512), 2 = 4x8x8 (256), -1 = per dtype
+#endif
+#ifndef MVN_X4_CORNER
+#define MVN_X4_CORNER 0  // 1: footprint boxes from the tile's corners (no barrier), else exact per voxel
+#endif
+#ifndef MVN_X4_ROWINT
+#define MVN_X4_ROWINT 0  // 1: chunks numbered over groups of 4 rows (conflict-free ds_write_b128)
+#endif
+
+namespace mvn {
+namespace unproj {
+namespace {
+
+// Voxel tile per block and LDS image size.  Tiles short in z project more compactly:
+// footprint slots per voxel at the bench configs 2.2 (4x8x16), 1.7 (8x8x8), 2.2 (4x8x8);
+// the largest footprints 2,156 / 1,428 / 965 slots (tools: /tmp-free model in DESIGN.md).
+template <int K> struct X4Shape;
+template <> struct X4Shape<0> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, MC = 2; };
+template <> struct X4Shape<1> { static constexpr int TX = 8, TY = 8, TZ = 8, THREADS = 512, SLOTS = 1536, MC = 2; };
+template <> struct X4Shape<2> { static constexpr int TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 1024, MC = 2; };
+
+template <int AGG, typename TIn, typename TOut, int K>
+__global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_per_eu(4))) void unproject_x4(
+    const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
+    const float* __restrict__ cub, int transfer, const float* __restrict__ conf, TOut* __restrict__ out, int B,
+    int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, int budget, int out_cl) {
+  constexpr int NV = 4, G = 4;
+  using S = X4Shape<K>;
+  constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ;
+  constexpr int kThreads = S::THREADS, kBuf = S::SLOTS, MC = S::MC, kWaves = kThreads / kWave;
+  static_assert(TX * TY * TZ == kThreads, "one voxel per thread");
+  // per buffer: image slots [0, kTrash), 64 per-lane trash slots (the masked-off pixels of
+  // a chunk are written there: no exec-mask branch per write), 2 zero slots
+  constexpr int kZeroSlot = kBuf - 2, kTrash = kBuf - 2 - kWave;
+  constexpr uint32_t kSlotB = 16;
+  constexpr uint32_t E = sizeof(TIn);
+
+  __shared__ uint4 stage[2 * kBuf];
+  __shared__ int red[kWaves][NV][4];
+
+  // ---- which tile (z-tiles fastest; block order as unproject_tiled) ------------------
+  const int nTx = (Vx + TX - 1) / TX, nTy = (Vy + TY - 1) / TY, nTz = (Vz + TZ - 1) / TZ;
+  int L = int(blockIdx.x);
+  {
+    const int nf = nTx * nTy * nTz;
+    if (B >= 16 && nf % 8 == 0) {
+      const int xcd = int(blockIdx.x) % 8, k = int(blockIdx.x) / 8, slab = nf / 8;
+      L = (k / slab) * nf + xcd * slab + k % slab;
+    }
+  }
+  const int tz = L % nTz; L /= nTz;
+  const int ty = L % nTy; L /= nTy;
+  const int tx = L % nTx;
+  const int b = L / nTx;
+
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int nvox = Vx * Vy * Vz;
+  const int HW = H * W;
+  X4_STAMP(0);
+  X4_STAMP(1);
+  const float* Pb = P + size_t(b) * NV * 12;
+  const TIn* fb = feat + size_t(b) * NV * C * HW;
+  const float* cfb = conf ? conf + size_t(b) * NV * C : nullptr;
+
+  if (t < 4) stage[(t >> 1) * kBuf + kZeroSlot + (t & 1)] = uint4{0u, 0u, 0u, 0u};
+
+  // ---- tile corners -> per-view footprint boxes (every wave for itself: no barrier) ----
+  // The voxel grid is an affine image of the integer lattice (a rotated cuboid,
+  // triangulation.py:280-341), and every voxel of the tile is in front of a camera whose
+  // 8 tile corners are: then the convex hull of the corners' projections contains every
+  // voxel's projection, so the bounding box of the corners (1e-3 px of slack for f32
+  // rounding) bounds the block's bilinear footprints.  Lanes 8v..8v+7 of lanes 0..31
+  // project corner (lane & 7) in view v.  Coordinate volumes that are not affine grids are
+  // caught per voxel below (a voxel outside its box is recomputed by global gathers); a
+  // tile that reaches behind a camera uses the exact per-voxel box (one barrier).
+  const int X0 = tx * TX, Y0 = ty * TY, Z0 = tz * TZ;
+  float cbox[4] = {0.f, 0.f, 0.f, 0.f};   // min x, max x, min y, max y (reduced over 8 lanes)
+  bool corner_ok = false;
+  if (MVN_X4_CORNER) {
+    const int c = lane & 7, v = (lane >> 3) & 3;
+    const int Xc = X0 + ((c & 4) ? min(TX, Vx - X0) - 1 : 0);
+    const int Yc = Y0 + ((c & 2) ? min(TY, Vy - Y0) - 1 : 0);
+    const int Zc = Z0 + ((c & 1) ? min(TZ, Vz - Z0) - 1 : 0);
+    float o[3];
+    if (cub) {
+      cuboid_coord(cub + b * MVN_CUBOID_FLOATS, Vx, Xc, Yc, Zc, transfer, o);
+    } else {
+      const float* cp = coords + (size_t(b) * nvox + (size_t(Xc) * Vy + Yc) * Vz + Zc) * 3;
+      o[0] = cp[0]; o[1] = cp[1]; o[2] = cp[2];
+    }
+    const Homog hp = homog(Pb + v * 12, o[0], o[1], o[2]);
+    const Recip rH0 = recip_refined(float(H)), rW0 = recip_refined(float(W));
+    const Proj pc = project_h<false>(hp, H, W, align_corners, rH0, rW0);
+    bool ok = (hp.wh > 0.f) & (fabsf(pc.ix) < 0x1p24f) & (fabsf(pc.iy) < 0x1p24f);
+    cbox[0] = pc.ix - 1e-3f; cbox[1] = pc.ix + 1e-3f; cbox[2] = pc.iy - 1e-3f; cbox[3] = pc.iy + 1e-3f;
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      cbox[0] = fminf(cbox[0], __shfl_xor(cbox[0], m, kWave));
+      cbox[1] = fmaxf(cbox[1], __shfl_xor(cbox[1], m, kWave));
+      cbox[2] = fminf(cbox[2], __shfl_xor(cbox[2], m, kWave));
+      cbox[3] = fmaxf(cbox[3], __shfl_xor(cbox[3], m, kWave));
+    }
+    corner_ok = (__builtin_amdgcn_ballot_w64(!ok) & 0xffffffffull) == 0;
+  }
+
+  // ---- this thread's voxel ------------------------------------------------------------
+  const int X = X0 + t / (TZ * TY), Y = Y0 + (t / TZ) % TY, Z = Z0 + t % TZ;
+  const bool act = (X < Vx) & (Y < Vy) & (Z < Vz);
+  const int vox = act ? (X * Vy + Y) * Vz + Z : 0;
+  float cx, cy, cz;
+  if (cub) {
+    float o[3];
+    cuboid_coord(cub + b * MVN_CUBOID_FLOATS, Vx, X, Y, Z, transfer, o);
+    cx = o[0]; cy = o[1]; cz = o[2];
+  } else {
+    const float* cp = coords + (size_t(b) * nvox + vox) * 3;
+    cx = cp[0]; cy = cp[1]; cz = cp[2];
+  }
+  int fx[NV], fy[NV];
+  float w[NV][4];
+  bool has[NV];
+  // per-voxel geometry: footprint base pixel, bilinear weights, "samples the image" flag
+  auto project_voxel = [&]() __attribute__((always_inline)) {
+    bool lane_fast = true;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) lane_fast &= div_core_safe(homog(Pb + v * 12, cx, cy, cz));
+    const bool wave_fast = __builtin_amdgcn_ballot_w64(!lane_fast) == 0;
+    const Recip rH = recip_refined(float(H)), rW = recip_refined(float(W));
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const Homog hp = homog(Pb + v * 12, cx, cy, cz);
+      const Proj p = wave_fast ? project_h<true>(hp, H, W, align_corners, rH, rW)
+                               : project_h<false>(hp, H, W, align_corners, rH, rW);
+      const float fx0 = floorf(p.ix), fy0 = floorf(p.iy);
+      const bool h = act & !p.invalid & (fx0 >= -1.f) & (fx0 < float(W)) & (fy0 >= -1.f) & (fy0 < float(H));
+      const float tx_ = p.ix - fx0, sx_ = 1.f - tx_, ty_ = p.iy - fy0, sy_ = 1.f - ty_;
+      w[v][0] = h ? sy_ * sx_ : 0.f; w[v][1] = h ? sy_ * tx_ : 0.f;
+      w[v][2] = h ? ty_ * sx_ : 0.f; w[v][3] = h ? ty_ * tx_ : 0.f;
+      fx[v] = h ? int(fx0) : 0; fy[v] = h ? int(fy0) : 0;
+      has[v] = h;
+    }
+  };
+
+  project_voxel();
+
+  // ---- per-view boxes (ints, clipped to the pixels a tap can start at) ----------------
+  int box[NV][4];
+  X4_STAMP(2);
+  if (MVN_X4_CORNER && corner_ok) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      box[v][0] = max(int(floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cbox[0]), 8 * v)))), -1);
+      box[v][1] = min(int(floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cbox[1]), 8 * v)))), W - 1);
+      box[v][2] = max(int(floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cbox[2]), 8 * v)))), -1);
+      box[v][3] = min(int(floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cbox[3]), 8 * v)))), H - 1);
+    }
+  } else {
+    // exact: every voxel's base pixel, DPP min / max per wave, combined over the waves
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int x0 = wave_min_u(has[v] ? fx[v] : INT_MAX), x1 = wave_max_u(has[v] ? fx[v] : INT_MIN);
+      const int y0 = wave_min_u(has[v] ? fy[v] : INT_MAX), y1 = wave_max_u(has[v] ? fy[v] : INT_MIN);
+      if (lane == 0) { red[wid][v][0] = x0; red[wid][v][1] = x1; red[wid][v][2] = y0; red[wid][v][3] = y1; }
+    }
+    __syncthreads();
+    int part;
+    {
+      const int v = (lane >> 2) & (NV - 1), k = lane & 3;
+      const bool mn = (k & 1) == 0;                           // components: x0 min, x1 max, y0 min, y1 max
+      part = mn ? INT_MAX : INT_MIN;
+#pragma unroll
+      for (int q = 0; q < kWaves; ++q) {
+        const int r = red[q][v][k];
+        part = mn ? min(part, r) : max(part, r);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) box[v][k] = __builtin_amdgcn_readlane(part, 4 * v + k);
+  }
+  X4_STAMP(3);
+
+  // ---- LDS regions (slots and chunks), in scalar registers ----------------------------
+  Region rg[NV];
+  int npass, total;
+  {
+    int snext = 0, cnext = 0, pass = 0, chunks0 = 0;
+    bool too_big = false;
+    const int lim = min(budget, kTrash);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      int x0 = box[v][0], y0 = box[v][2];
+      const int x1 = box[v][1], y1 = box[v][3];
+      int bw = 0, bh = 0;
+      if (x0 <= x1 && y0 <= y1) { bw = x1 - x0 + 2; bh = y1 - y0 + 2; }   // +1 px: east / south taps
+      else { x0 = 0; y0 = 0; }
+      const int pitch = bw | 1;                                 // odd: spreads rows over banks
+      const int xa = x0 & ~3;                                   // chunk origin, x % 4 == 0
+      const int cw = bw ? (x0 + bw - xa + 3) >> 2 : 0;          // chunks per row
+      // chunks are numbered over groups of 4 rows, rows fastest (see chunk_fields): rows
+      // padded to a multiple of 4
+      const int area = pitch * bh, nch = cw * (MVN_X4_ROWINT ? (bh + 3) & ~3 : bh);
+      if (area > lim || nch > MC * kThreads) too_big = true;
+      if (snext + area > lim || cnext + nch > MC * kThreads) { ++pass; snext = 0; cnext = 0; }
+      rg[v].x0 = x0; rg[v].y0 = y0; rg[v].bw = bw; rg[v].bh = bh; rg[v].pitch = pitch; rg[v].sbase = snext;
+      rg[v].xa = xa; rg[v].cw = cw; rg[v].cbase = cnext; rg[v].pass = pass; rg[v].cend = cnext + nch;
+      rg[v].inv_cw = cw ? __builtin_amdgcn_rcpf(float(cw)) : 0.f;
+      snext += area;
+      cnext += nch;
+      if (pass == 0) chunks0 = cnext;
+    }
+    npass = too_big ? -1 : pass + 1;
+    total = chunks0;
+  }
+  X4_STAMP(4);
+
+  if (npass < 0) {
+    // A single view's footprint exceeds the LDS buffer: gather straight from global memory.
+    if (act)
+      gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + (out_cl ? size_t(vox) * C : vox),
+                                   out_cl ? 1 : nvox, NV, C, H, W, cx, cy, cz, align_corners);
+    return;
+  }
+
+  const __amdgpu_buffer_rsrc_t frs = make_rsrc(fb, uint32_t(size_t(NV) * C * HW * E));
+  const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + size_t(b) * C * nvox, uint32_t(size_t(C) * nvox * sizeof(TOut)));
+  const uint32_t ooff = act ? uint32_t(vox) * uint32_t(sizeof(TOut)) : kOob;
+  const uint32_t ooff_cl = act ? uint32_t(vox) * uint32_t(C) * uint32_t(sizeof(TOut)) : kOob;
+
+  // LDS byte offsets of each view's north-west and south-west taps; a voxel whose base
+  // pixel falls outside its view's box (only possible for a coordinate volume that is not
+  // an affine grid) samples the zero slots and is recomputed by global gathers at the end.
+  uint32_t anw[NV], asw[NV];
+  bool refix = false;
+  auto tap_slots = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int dx = fx[v] - rg[v].x0, dy = fy[v] - rg[v].y0;
+      // (exact boxes contain every voxel's base pixel by construction)
+      const bool inbox = !MVN_X4_CORNER || ((dx >= 0) & (dx <= rg[v].bw - 2) & (dy >= 0) & (dy <= rg[v].bh - 2));
+      if (MVN_X4_CORNER) refix |= has[v] & !inbox;             // (has implies act)
+      const bool use = has[v] & inbox;
+      const int slot = rg[v].sbase + dy * rg[v].pitch + dx;
+      anw[v] = uint32_t(use ? slot : kZeroSlot) * kSlotB;
+      asw[v] = uint32_t(use ? slot + rg[v].pitch : kZeroSlot) * kSlotB;
+      if (MVN_X4_ABL_BCAST) {
+        anw[v] = __builtin_amdgcn_readfirstlane(anw[v]);
+        asw[v] = __builtin_amdgcn_readfirstlane(asw[v]);
+      }
+    }
+  };
+  // (coordinates re-derived here, so that nothing of the prologue stays live through the
+  // channel loop for this rare path)
+  auto fix_voxel = [&]() __attribute__((always_inline)) {
+    if (MVN_X4_CORNER && refix) {
+      const int Xr = X0 + int(threadIdx.x) / (TZ * TY), Yr = Y0 + (int(threadIdx.x) / TZ) % TY;
+      const int Zr = Z0 + int(threadIdx.x) % TZ;
+      const int vr = (Xr * Vy + Yr) * Vz + Zr;
+      float o[3];
+      if (cub) {
+        cuboid_coord(cub + b * MVN_CUBOID_FLOATS, Vx, Xr, Yr, Zr, transfer, o);
+      } else {
+        const float* cp = coords + (size_t(b) * nvox + vr) * 3;
+        o[0] = cp[0]; o[1] = cp[1]; o[2] = cp[2];
+      }
+      gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + (out_cl ? size_t(vr) * C : vr),
+                                   out_cl ? 1 : nvox, NV, C, H, W, o[0], o[1], o[2], align_corners);
+    }
+  };
+
+  // Chunk (k of a pass) -> global byte offset (kOob outside the image), first LDS slot and
+  // the mask of its 4 pixels that lie in the view's box (empty past the pass's chunks).
+  auto chunk_fields = [&](const Region& r, int sel, int li, uint32_t& goff, int& s0, uint32_t& mask, bool live)
+      __attribute__((always_inline)) {
+    // li = (row group * cw + chunk column) * 4 + row in group: the 8 lanes of a
+    // ds_write_b128 lane group then cover 4 rows x 2 chunks, whose slots differ by an odd
+    // pitch between rows and by 4 between chunks — 8 distinct 16-byte bank groups, where
+    // 8 chunks of one row would hit only two (4-way conflicts).
+#if MVN_X4_ROWINT
+    const int q = li >> 2;
+    const int grp = int((float(q) + 0.5f) * r.inv_cw);
+    const int py = 4 * grp + (li & 3);
+    live &= py < r.bh;
+    const int gx = r.xa + 4 * (q - grp * r.cw), gy = r.y0 + py;
+#else
+    const int py = int((float(li) + 0.5f) * r.inv_cw);
+    const int gx = r.xa + 4 * (li - py * r.cw), gy = r.y0 + py;
+#endif
+    const bool in = live & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
+    goff = in ? uint32_t((sel * C * HW + gy * W + gx) * int(E)) : kOob;
+    s0 = r.sbase + py * r.pitch + (gx - r.x0);
+    mask = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int dx = gx + p - r.x0;
+      mask |= (live & (dx >= 0) & (dx < r.bw)) ? (1u << p) : 0u;
+    }
+  };
+  using Chunk = typename ChunkT<TIn>::type;
+  auto load_group = [&](Chunk (&pre)[G], uint32_t goff, int c0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < G; ++k) pre[k] = load_chunk<TIn>(frs, goff, uint32_t((c0 + k) * HW) * E);
+  };
+  // masked-off pixels: bf16 maps write them to the lane's trash slot (no exec-mask branch
+  // per write), f32 maps branch (A/B at the bench configs: each is the faster for its dtype)
+  auto write_group = [&](uint4* buf, const Chunk (&pre)[G], int s0, uint32_t mask) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const uint4 q = make_uint4(chunk_px(pre[0], p), chunk_px(pre[1], p), chunk_px(pre[2], p), chunk_px(pre[3], p));
+      if constexpr (sizeof(TIn) == 2)
+        buf[(mask & (1u << p)) ? s0 + p : kTrash + lane] = q;
+      else if (mask & (1u << p))
+        buf[s0 + p] = q;
+    }
+  };
+
+  // sample the views staged in an LDS buffer (all, or those of `pass`) into channel pairs
+  auto sample_views = [&](const char* buf, bool all, int pass, f2 (&sv)[2][NV]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (!all && rg[v].pass != pass) continue;
+      const uint4 a = *reinterpret_cast<const uint4*>(buf + anw[v]);
+      const uint4 bq = *reinterpret_cast<const uint4*>(buf + anw[v] + kSlotB);
+      const uint4 cq = *reinterpret_cast<const uint4*>(buf + asw[v]);
+      const uint4 d = *reinterpret_cast<const uint4*>(buf + asw[v] + kSlotB);
+      const f2 w0{w[v][0], w[v][0]}, w1{w[v][1], w[v][1]}, w2{w[v][2], w[v][2]}, w3{w[v][3], w[v][3]};
+      sv[0][v] = pk_fma(lo2(d), w3, pk_fma(lo2(cq), w2, pk_fma(lo2(bq), w1, lo2(a) * w0)));
+      sv[1][v] = pk_fma(hi2(d), w3, pk_fma(hi2(cq), w2, pk_fma(hi2(bq), w1, hi2(a) * w0)));
+      if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight
+    }
+  };
+  auto aggregate_store = [&](int c0, const f2 (&sv)[2][NV]) __attribute__((always_inline)) {
+    float r[G];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      f2 cf[NV];
+      if constexpr (AGG == MVN_AGG_CONF) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) cf[v] = f2{cfb[v * C + c0 + 2 * q], cfb[v * C + c0 + 2 * q + 1]};
+      }
+      const f2 o = aggregate_pair<AGG>(sv[q], cf);
+      r[2 * q] = o.x;
+      r[2 * q + 1] = o.y;
+    }
+    if (out_cl) {
+      const uint32_t soff = uint32_t(c0) * uint32_t(sizeof(TOut));
+      if constexpr (sizeof(TOut) == 4)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
+                               make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]),
+                                          __float_as_uint(r[3]))),
+            ors, ooff_cl, soff, 0);
+      else
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int,
+                               make_uint2(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[2], r[3]))),
+            ors, ooff_cl, soff, 0);
+      return;
+    }
+#pragma unroll
+    for (int ch = 0; ch < G; ++ch)
+      if (!MVN_X4_ABL_NOSTORE || r[ch] == 1234.5f)
+        store_plane<TOut>(r[ch], ors, ooff, uint32_t(c0 + ch) * uint32_t(nvox) * uint32_t(sizeof(TOut)));
+  };
+
+  auto consume = [&](const uint4* buf, int c0) __attribute__((always_inline)) {
+    f2 sv[2][NV];
+    sample_views(reinterpret_cast<const char*>(buf), true, 0, sv);
+    aggregate_store(c0, sv);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (npass == 1) {
+    // ---- one pass: up to MC chunks per thread (chunk t + kThreads * i over the views'
+    // concatenated chunk ranges), two LDS buffers, the next group's loads in flight --------
+    uint32_t goff[MC], mask[MC];
+    int s0[MC];
+#pragma unroll
+    for (int i = 0; i < MC; ++i) {
+      const int k = t + kThreads * i;
+      int sel = 0;
+#pragma unroll
+      for (int u = 1; u < NV; ++u)
+        if (rg[u].cw > 0 && k >= rg[u].cbase) sel = u;
+      const Region r = pick_region(rg, sel);
+      chunk_fields(r, sel, k - r.cbase, goff[i], s0[i], mask[i], k < total);
+    }
+    const int wfirst = __builtin_amdgcn_readfirstlane(wid * kWave);
+    Chunk pre[MC][G];
+    auto issue = [&](int c0) __attribute__((always_inline)) {
+      if (MVN_X4_ABL_NOSTAGE && c0 >= 2 * G) return;
+#pragma unroll
+      for (int i = 0; i < MC; ++i)
+        if (wfirst + kThreads * i < total) load_group(pre[i], goff[i], c0);
+    };
+    int ncommit = 0;
+    auto commit = [&](uint4* buf) __attribute__((always_inline)) {
+      if (MVN_X4_ABL_NOSTAGE && ncommit++ >= 2) return;
+#pragma unroll
+      for (int i = 0; i < MC; ++i)
+        if (wfirst + kThreads * i < total) write_group(buf, pre[i], s0[i], mask[i]);
+    };
+    issue(0);
+    X4_STAMP(5);
+    tap_slots();
+    commit(stage);
+    __syncthreads();
+    X4_STAMP(6);
+    X4_ACC_DECL;
+    for (int c0 = 0; c0 < C; c0 += 2 * G) {
+      const bool more1 = c0 + G < C, more2 = c0 + 2 * G < C;
+      if (more1) issue(c0 + G);
+      X4_ACC(3);
+      consume(stage, c0);
+      X4_ACC(0);
+      if (!more1) break;
+      commit(stage + kBuf);
+      X4_ACC(1);
+      __syncthreads();
+      X4_ACC(2);
+      if (more2) issue(c0 + 2 * G);
+      X4_ACC(3);
+      consume(stage + kBuf, c0 + G);
+      X4_ACC(0);
+      if (!more2) break;
+      commit(stage);
+      X4_ACC(1);
+      __syncthreads();
+      X4_ACC(2);
+    }
+    X4_STAMP(7);
+    X4_ACC_STORE;
+    fix_voxel();
+    return;
+  }
+
+  // ---- several passes of whole views per channel group (close cameras) ---------------
+  tap_slots();
+  for (int c0 = 0; c0 < C; c0 += G) {
+    f2 sv[2][NV];
+    for (int pass = 0; pass < npass; ++pass) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {          // every thread stages chunks of each view of the pass
+        if (rg[v].pass != pass) continue;
+        const int nch = rg[v].cend - rg[v].cbase;
+        for (int li = t; li < nch; li += kThreads) {
+          uint32_t goff, mask;
+          int s0;
+          chunk_fields(rg[v], v, li, goff, s0, mask, true);
+          Chunk pre[G];
+          load_group(pre, goff, c0);
+          write_group(stage, pre, s0, mask);
+        }
+      }
+      __syncthreads();
+      sample_views(reinterpret_cast<const char*>(stage), false, pass, sv);
+      __syncthreads();
+    }
+    aggregate_store(c0, sv);
+  }
+  fix_voxel();
+}
+
+}  // namespace
+
+#if MVN_X4_STAMPS
+extern "C" int mvn_x4_stamps(void* dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_x4_stamps), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
+
+// Returns MVN_OK, an error code, or 1 when this kernel does not apply (the caller then
+// runs unproject_tiled).
+template <int AGG, typename TIn, typename TOut>
+int launch_x4(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
+              const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+              int align_corners, int out_cl, hipStream_t s) {
+  if (N != 4 || W % 4 != 0 || C % 4 != 0) return 1;
+  if (MVN_USE_W4)
+    return launch_w4<AGG, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz,
+                                     align_corners, out_cl, s);
+  if ((long long)N * C * H * W * sizeof(TIn) >= (1LL << 31) ||
+      (long long)C * Vx * Vy * Vz * sizeof(TOut) >= (1LL << 31))
+    return MVN_ERR_SHAPE;
+  const int knob = unproject_lds_slot_budget();
+  const int budget = knob > 0 ? knob : 1 << 30;
+  // tile per input dtype (A/B at the bench configs): f32 4x8x16, bf16 4x8x8
+  constexpr int K = MVN_X4_TILE >= 0 ? MVN_X4_TILE : (sizeof(TIn) == 2 ? 2 : 0);
+  using S = X4Shape<K>;
+  const long long nb = (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) *
+                       ((Vz + S::TZ - 1) / S::TZ);
+  if (nb > INT_MAX) return MVN_ERR_SHAPE;
+  unproject_x4<AGG, TIn, TOut, K><<<int(nb), S::THREADS, 0, s>>>(
+      static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, C, H, W, Vx, Vy,
+      Vz, align_corners, budget, out_cl);
+  return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
+}
+
+#define MVN_INSTANTIATE(AGG)                                                                                   \
+  template int launch_x4<AGG, float, float>(const void*, const float*, const float*, const float*, int,        \
+                                            const float*, void*, int, int, int, int, int, int, int, int, int,  \
+                                            int, hipStream_t);                                                 \
+  template int launch_x4<AGG, uint16_t, uint16_t>(const void*, const float*, const float*, const float*, int,  \
+                                                  const float*, void*, int, int, int, int, int, int, int, int, \
+                                                  int, int, hipStream_t);                                      \
+  template int launch_x4<AGG, uint16_t, float>(const void*, const float*, const float*, const float*, int,     \
+                                               const float*, void*, int, int, int, int, int, int, int, int,    \
+                                               int, int, hipStream_t);
+MVN_INSTANTIATE(MVN_AGG_SUM)
+MVN_INSTANTIATE(MVN_AGG_MAX)
+MVN_INSTANTIATE(MVN_AGG_SOFTMAX)
+MVN_INSTANTIATE(MVN_AGG_CONF)
+#undef MVN_INSTANTIATE
+
+}  // namespace unproj
+}  // namespace mvn

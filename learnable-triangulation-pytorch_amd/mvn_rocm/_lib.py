@@ -90,8 +90,8 @@ class unproject_knobs:
     """Context manager (tests only): force unprojection paths through the C ABI's test hook
     ``mvn_debug_set_unproject`` and restore the defaults on exit."""
 
-    def __init__(self, lds_slots: int = 0, simple: bool = False):
-        self.args = (int(lds_slots), int(bool(simple)))
+    def __init__(self, lds_slots: int = 0, simple: bool = False, generic: bool = False):
+        self.args = (int(lds_slots), 1 if simple else 2 if generic else 0)
 
     def __enter__(self):
         check(load().mvn_debug_set_unproject(*self.args), "mvn_debug_set_unproject")

@@ -1,0 +1,118 @@
+"""The four-view unprojection kernel (csrc/unproject_x4.hip: chunked staging, packed f32
+arithmetic) against the generic tiled kernel (bit for bit, every aggregation, dtype and
+layout) and against the C oracle, on every staging path (one LDS pass, several passes,
+global-gather fallback) and on coordinate volumes that are not affine grids.  MI355X only."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import max_rel
+from oracle import capi
+
+pytestmark = pytest.mark.gpu
+
+METHODS = ("sum", "max", "softmax", "conf")
+
+
+def _bits(t):
+    return t.contiguous().view(torch.int32) if t.dtype == torch.float32 else t.contiguous().view(torch.int16)
+
+
+def _run(vb_feat, proj, coords, method, conf, out_dtype=None, **knobs):
+    from mvn_rocm import _lib, op
+    with _lib.unproject_knobs(**knobs):
+        return op.unproject_heatmaps(vb_feat, proj, coords, method, conf, out_dtype=out_dtype)
+
+
+def _batch(device, seed, heatmap=64, volume=32, channels=8, dtype=torch.float32):
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(2, n_views=4, channels=channels, heatmap=heatmap, volume=volume, seed=seed)
+    conf = torch.from_numpy(np.random.default_rng(seed).uniform(0.05, 1.0, (2, 4, channels)).astype(np.float32))
+    return vb, conf
+
+
+@pytest.mark.parametrize("method", METHODS)
+@pytest.mark.parametrize("dt", ("f32", "bf16", "bf16->f32"))
+def test_x4_equals_generic_kernel_and_oracle(device, method, dt):
+    vb, conf = _batch(device, 70)
+    feat = vb.features.to(device)
+    od = None
+    if dt != "f32":
+        feat = feat.to(torch.bfloat16)
+        od = torch.float32 if dt == "bf16->f32" else None
+    P, X, cf = vb.proj.to(device), vb.coords.to(device), conf.to(device)
+    a = _run(feat, P, X, method, cf, od)
+    b = _run(feat, P, X, method, cf, od, generic=True)
+    assert torch.equal(_bits(a), _bits(b))
+    bits = feat.cpu().view(torch.int16).numpy().view(np.uint16) if feat.dtype == torch.bfloat16 else None
+    ref = capi.unproject(bits if bits is not None else vb.features.numpy(), vb.proj.numpy(), vb.coords.numpy(),
+                         method, conf.numpy(), feat_bf16_bits=bits is not None)
+    got = a.float().cpu().numpy()
+    if a.dtype == torch.bfloat16:
+        np.testing.assert_allclose(got, ref, rtol=2 ** -8, atol=2 ** -8 * np.abs(ref).max())
+    elif method == "softmax":
+        assert max_rel(got, ref) <= 1e-5
+    else:
+        np.testing.assert_array_equal(got, ref)
+
+
+def _tile_areas(proj, coords, H, W, tile=(4, 8, 16)):
+    from test_gpu_parity import tile_footprints
+    return tile_footprints(proj, coords, H, W, tile)
+
+
+@pytest.mark.parametrize("path", ("multipass", "fallback"))
+@pytest.mark.parametrize("method", ("sum", "softmax"))
+def test_x4_staging_paths(device, path, method):
+    """LDS budgets that force several staging passes of whole views, and single views
+    larger than the budget (global-gather fallback) — against the oracle."""
+    vb, conf = _batch(device, 71, heatmap=64, volume=32, channels=8)
+    areas = _tile_areas(vb.proj.numpy(), vb.coords.numpy(), 64, 64)
+    if path == "multipass":
+        budget = int(areas.max()) + 64
+        assert (areas.sum(1) + 1 > budget).any()
+    else:
+        budget = int(np.median(areas[areas > 0]))
+        assert (areas.max(1) > budget - 1).any() and (areas.max(1) <= budget - 1).any()
+    out = _run(vb.features.to(device), vb.proj.to(device), vb.coords.to(device), method, None, lds_slots=budget)
+    ref = capi.unproject(vb.features.numpy(), vb.proj.numpy(), vb.coords.numpy(), method)
+    if method == "softmax":
+        assert max_rel(out.cpu().numpy(), ref) <= 1e-5
+    else:
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("method", ("sum", "softmax"))
+def test_x4_non_affine_coordinates(device, method):
+    """op.py:99 accepts ANY coordinate volume: jittered and shuffled voxel coordinates (not
+    an affine grid) must still match the oracle."""
+    vb, _ = _batch(device, 72, heatmap=64, volume=32, channels=8)
+    rng = np.random.default_rng(72)
+    X = vb.coords.numpy().copy()
+    X += rng.normal(0, 40.0, X.shape).astype(np.float32)               # jitter (~1 voxel)
+    flat = X.reshape(2, -1, 3)
+    for b in range(2):                                                   # a few far-flung voxels
+        idx = rng.choice(flat.shape[1], 200, replace=False)
+        flat[b, idx] = flat[b, rng.permutation(idx)]
+    out = _run(vb.features.to(device), vb.proj.to(device), torch.from_numpy(X).to(device), method, None)
+    ref = capi.unproject(vb.features.numpy(), vb.proj.numpy(), X, method)
+    if method == "softmax":
+        assert max_rel(out.cpu().numpy(), ref) <= 1e-5
+    else:
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("dt", (torch.float32, torch.bfloat16))
+def test_x4_channels_last_and_cuboids_equal_generic(device, dt):
+    """Channels-last output (config 5) and in-kernel cuboid coordinates through the
+    four-view kernel, bit-identical to the generic kernel."""
+    from mvn_rocm import _lib, synth, v2v, volumetric
+    vb = synth.volumetric_batch(2, n_views=4, channels=32, heatmap=96, volume=8, seed=73)
+    rng = np.random.default_rng(73)
+    base = rng.uniform(-500, 500, (2, 3)) + np.array([0, 0, 900.0])
+    cub = volumetric.build_cuboids(base, 2500.0, 32, rng.uniform(0, 2 * np.pi, 2), "coco", False, device=device)
+    feat, P = vb.features.to(device).to(dt), vb.proj.to(device)
+    a = v2v.unproject_channels_last(feat, P, cub, "softmax", out_dtype=dt)
+    with _lib.unproject_knobs(generic=True):
+        b = v2v.unproject_channels_last(feat, P, cub, "softmax", out_dtype=dt)
+    assert torch.equal(_bits(a), _bits(b))

@@ -161,7 +161,7 @@ def measured_traffic(cfg_name):
         return None, None
     data = json.load(open(files[-1]))
     for k, d in data.get(f"cfg{cfg_name}", {}).items():
-        if k.startswith("unproject_tiled<2,") and "hbm_bytes_per_launch" in d:
+        if k.startswith(("unproject_x4<2,", "unproject_tiled<2,")) and "hbm_bytes_per_launch" in d:
             return d["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
     return None, None
 
@@ -169,7 +169,9 @@ def measured_traffic(cfg_name):
 def kernel_name(c):
     import torch
     t = "float" if c["dtype"] == torch.float32 else "bf16"
-    return f"unproject_tiled<softmax, {t}, {t}, {4 if c['views'] <= 4 else 8} views>"
+    if c["views"] == 4:      # the four-view kernel (csrc/unproject_x4.hip), tile per dtype
+        return f"unproject_x4<softmax, {t}, {t}, tile {'4x8x16' if t == 'float' else '4x8x8'}>"
+    return f"unproject_tiled<softmax, {t}, {t}, 8 views>"
 
 
 def dtype_name(dt):

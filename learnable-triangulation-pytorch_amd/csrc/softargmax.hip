@@ -174,12 +174,8 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     for (int r = 0; r < RUNS; ++r)
       load_run<T, VEC>(vb + j * jstride, chunk * kPartChunk + r * kWave * VEC + lane * VEC, nvox, vec_ok, x[r], fill);
   };
-
-  float x[RUNS][VEC];
-  load(0, x);
-  for (int j = 0; j < J; ++j) {
-    float xn[RUNS][VEC];
-    if (j + 1 < J) load(j + 1, xn);
+  // One joint's 5-float partial from its (multiplier-scaled) values.
+  auto reduce_joint = [&](int j, float (&x)[RUNS][VEC]) __attribute__((always_inline)) {
     float m = 0.f, s = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
     if constexpr (SOFTMAX) {
       constexpr float kLog2e = 1.4426950408889634f;
@@ -219,6 +215,57 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
       float* o = part + ((size_t(b) * J + j) * nchunk + chunk) * kPartial;
       o[0] = m; o[1] = s; o[2] = sx; o[3] = sy; o[4] = sz;
     }
+  };
+
+  const int i0 = chunk * kPartChunk + lane * VEC;
+  if (vec_ok && chunk * kPartChunk + kPartChunk <= nvox) {
+    // Full chunk, aligned: the raw 16-byte loads of PF joints in flight (a ring of register
+    // sets refilled PF joints ahead), widened only when their joint is reduced.  One joint
+    // ahead left the loads' latency exposed (the volume was just written by the
+    // unprojection and streams from HBM): 2.5 TB/s at config 3 in r06.
+    constexpr int PF = sizeof(T) == 2 ? 8 : 4;
+    uint4 raw[PF][RUNS];
+    auto issue = [&](int j, uint4 (&q)[RUNS]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int r = 0; r < RUNS; ++r)
+        q[r] = *reinterpret_cast<const uint4*>(vb + j * jstride + i0 + r * kWave * VEC);
+    };
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+      if (p < J) issue(p, raw[p]);
+    for (int j0 = 0; j0 < J; j0 += PF) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        const int j = j0 + p;
+        if (j >= J) break;
+        float x[RUNS][VEC];
+#pragma unroll
+        for (int r = 0; r < RUNS; ++r) {
+          const uint32_t w[4] = {raw[p][r].x, raw[p][r].y, raw[p][r].z, raw[p][r].w};
+          if constexpr (sizeof(T) == 4) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[r][k] = __uint_as_float(w[k]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              x[r][2 * k] = __uint_as_float(w[k] << 16);
+              x[r][2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+            }
+          }
+        }
+        if (j + PF < J) issue(j + PF, raw[p]);
+        reduce_joint(j, x);
+      }
+    }
+    return;
+  }
+
+  float x[RUNS][VEC];
+  load(0, x);
+  for (int j = 0; j < J; ++j) {
+    float xn[RUNS][VEC];
+    if (j + 1 < J) load(j + 1, xn);
+    reduce_joint(j, x);
     if (j + 1 < J) {
 #pragma unroll
       for (int r = 0; r < RUNS; ++r)

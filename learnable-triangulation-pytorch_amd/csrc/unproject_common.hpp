@@ -268,7 +268,7 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
                  const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
                  int align_corners, int out_cl, hipStream_t s);
 
-// ---- helpers of the four-view kernels (unproject_x4.hip, unproject_w4.hip) ------------
+// ---- helpers of the four-view kernel (unproject_x4.hip) --------------------------------
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
@@ -369,12 +369,6 @@ __device__ __forceinline__ Region pick_region(const Region (&rg)[4], int u) {
   return r;
 }
 
-
-// The wave-autonomous four-view kernel (unproject_w4.hip), same contract as launch_x4.
-template <int AGG, typename TIn, typename TOut>
-int launch_w4(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
-              const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
-              int align_corners, int out_cl, hipStream_t s);
 
 // The four-view kernel (unproject_x4.hip): MVN_OK, an error code, or 1 when it does not
 // apply to the call (then launch_tiled runs the generic kernel).

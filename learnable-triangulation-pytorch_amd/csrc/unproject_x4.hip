@@ -67,9 +67,6 @@ __device__ unsigned long long g_x4_stamps[1 << 21];
 #define X4_ACC_STORE do {} while (0)
 #endif
 
-#ifndef MVN_USE_W4
-#define MVN_USE_W4 0     // 1: four-view calls go to the wave-autonomous kernel (unproject_w4.hip)
-#endif
 #ifndef MVN_X4_TILE
 #define MVN_X4_TILE -1   // voxel tile: 0 = 4x8x16 (512 threads), 1 = 8x8x8 (512), 2 = 4x8x8 (256), -1 = per dtype
 #endif
@@ -88,12 +85,20 @@ namespace {
 // footprint slots per voxel at the bench configs 2.2 (4x8x16), 1.7 (8x8x8), 2.2 (4x8x8);
 // the largest footprints 2,156 / 1,428 / 965 slots (tools: /tmp-free model in DESIGN.md).
 template <int K> struct X4Shape;
-template <> struct X4Shape<0> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, MC = 2; };
-template <> struct X4Shape<1> { static constexpr int TX = 8, TY = 8, TZ = 8, THREADS = 512, SLOTS = 1536, MC = 2; };
-template <> struct X4Shape<2> { static constexpr int TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 1024, MC = 2; };
+template <> struct X4Shape<0> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, MC = 2, WAVES = 4; };
+template <> struct X4Shape<1> { static constexpr int TX = 8, TY = 8, TZ = 8, THREADS = 512, SLOTS = 1536, MC = 2, WAVES = 4; };
+#ifndef MVN_X4_T2_SLOTS
+#define MVN_X4_T2_SLOTS 1024
+#endif
+#ifndef MVN_X4_T2_WAVES
+#define MVN_X4_T2_WAVES 4
+#endif
+template <> struct X4Shape<2> {
+  static constexpr int TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = MVN_X4_T2_SLOTS, MC = 2, WAVES = MVN_X4_T2_WAVES;
+};
 
 template <int AGG, typename TIn, typename TOut, int K>
-__global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_per_eu(4))) void unproject_x4(
+__global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_per_eu(X4Shape<K>::WAVES))) void unproject_x4(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ cub, int transfer, const float* __restrict__ conf, TOut* __restrict__ out, int B,
     int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, int budget, int out_cl) {
@@ -550,9 +555,6 @@ int launch_x4(const void* feat, const float* P, const float* coords, const float
               const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
               int align_corners, int out_cl, hipStream_t s) {
   if (N != 4 || W % 4 != 0 || C % 4 != 0) return 1;
-  if (MVN_USE_W4)
-    return launch_w4<AGG, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz,
-                                     align_corners, out_cl, s);
   if ((long long)N * C * H * W * sizeof(TIn) >= (1LL << 31) ||
       (long long)C * Vx * Vy * Vz * sizeof(TOut) >= (1LL << 31))
     return MVN_ERR_SHAPE;

@@ -19,7 +19,8 @@ for cfg in 2 3; do
   done
 done
 echo "traffic passes done"
-bash tools/pmc_sq.sh "$out/sq_cfg2" 'unproject_tiled' python3 tools/prof_unproject.py 2 5
+bash tools/pmc_sq.sh "$out/sq_cfg2" 'unproject_x4' python3 tools/prof_unproject.py 2 5
+bash tools/pmc_sq.sh "$out/sq_cfg3" 'unproject_x4' python3 tools/prof_unproject.py 3 5
 echo "sq passes done"
 bash tools/pmc_cycles.sh "$out/v2v_cycles" learnable-triangulation-pytorch_amd/mvn_rocm/libmvn_hip.so > "$out/v2v_cycles.txt" 2>&1
 echo "v2v cycle pass done"

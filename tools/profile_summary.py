@@ -57,19 +57,22 @@ traffic["_note"] = ("rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passe
                     "HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), MI355X_MICROARCH.md 'HBM' gfx950 rule")
 json.dump(traffic, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1, sort_keys=True)
 
-# 3. SQ mix
-vals = defaultdict(lambda: defaultdict(list))
-for f in glob.glob(os.path.join(raw, "sq_cfg2", "p*", "**", "*counter_collection.csv"), recursive=True):
-    for r in csv.DictReader(open(f)):
-        vals[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
-with open(os.path.join(dst, f"{tag}_sq_cfg2.txt"), "w") as fo:
-    for k, d in vals.items():
-        fo.write(k + "\n")
-        waves = sum(d["SQ_WAVES"]) / len(d["SQ_WAVES"]) if "SQ_WAVES" in d else None
-        for c in sorted(d):
-            m = sum(d[c]) / len(d[c])
-            per = f"   per wave {m / waves:12.1f}" if waves else ""
-            fo.write(f"   {c:28s} {m:16.1f}{per}\n")
+# 3. SQ mix (configs 2 and 3)
+for cfg in ("2", "3"):
+    vals = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(raw, f"sq_cfg{cfg}", "p*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            vals[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    if not vals:
+        continue
+    with open(os.path.join(dst, f"{tag}_sq_cfg{cfg}.txt"), "w") as fo:
+        for k, d in vals.items():
+            fo.write(k + "\n")
+            waves = sum(d["SQ_WAVES"]) / len(d["SQ_WAVES"]) if "SQ_WAVES" in d else None
+            for c in sorted(d):
+                m = sum(d[c]) / len(d[c])
+                per = f"   per wave {m / waves:12.1f}" if waves else ""
+                fo.write(f"   {c:28s} {m:16.1f}{per}\n")
 print(open(os.path.join(dst, f"{tag}_kernel_stats.csv")).read())
 print(json.dumps(traffic, indent=1))
-print(open(os.path.join(dst, f"{tag}_sq_cfg2.txt")).read())
+

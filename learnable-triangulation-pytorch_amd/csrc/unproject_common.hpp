@@ -268,7 +268,7 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
                  const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
                  int align_corners, int out_cl, hipStream_t s);
 
-// ---- helpers of the four-view kernel (unproject_x4.hip) --------------------------------
+// ---- helpers of the chunk-staged kernel (unproject_x4.hip) ------------------------------
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
@@ -302,15 +302,18 @@ __device__ __forceinline__ f2 lo2(const uint4& q) { return f2{__uint_as_float(q.
 __device__ __forceinline__ f2 hi2(const uint4& q) { return f2{__uint_as_float(q.z), __uint_as_float(q.w)}; }
 
 // View aggregation of a channel pair (op.py:147-161), lane-wise the op order of
-// aggregate<> (sum / max / conf, reference order) and of aggregate_fast<> (softmax).
-template <int AGG>
-__device__ __forceinline__ f2 aggregate_pair(const f2 (&s)[4], const f2 (&cf)[4]) {
+// aggregate<> (sum / max / conf, reference order; softmax, the unified formula).
+template <int AGG, int NV>
+__device__ __forceinline__ f2 aggregate_pair(const f2 (&s)[NV], const f2 (&cf)[NV]) {
   if constexpr (AGG == MVN_AGG_SUM) {
-    return ((s[0] + s[1]) + s[2]) + s[3];
+    f2 r = s[0];
+#pragma unroll
+    for (int v = 1; v < NV; ++v) r = r + s[v];
+    return r;
   } else if constexpr (AGG == MVN_AGG_MAX) {
     f2 r = s[0];
 #pragma unroll
-    for (int v = 1; v < 4; ++v) {
+    for (int v = 1; v < NV; ++v) {
       r.x = s[v].x > r.x ? s[v].x : r.x;
       r.y = s[v].y > r.y ? s[v].y : r.y;
     }
@@ -318,24 +321,31 @@ __device__ __forceinline__ f2 aggregate_pair(const f2 (&s)[4], const f2 (&cf)[4]
   } else if constexpr (AGG == MVN_AGG_CONF) {
     f2 r = s[0] * cf[0];
 #pragma unroll
-    for (int v = 1; v < 4; ++v) r = r + s[v] * cf[v];
+    for (int v = 1; v < NV; ++v) r = r + s[v] * cf[v];
     return r;
   } else {
     constexpr float kLog2e = 1.4426950408889634f;
-    f2 m;
-    m.x = fmaxf(fmaxf(fmaxf(s[0].x, s[1].x), s[2].x), s[3].x);
-    m.y = fmaxf(fmaxf(fmaxf(s[0].y, s[1].y), s[2].y), s[3].y);
-    const f2 nml = -(m * f2{kLog2e, kLog2e});
-    f2 e[4];
+    f2 m = s[0];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 1; v < NV; ++v) {
+      m.x = fmaxf(m.x, s[v].x);
+      m.y = fmaxf(m.y, s[v].y);
+    }
+    const f2 nml = -(m * f2{kLog2e, kLog2e});
+    f2 e[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
       const f2 a = pk_fma(s[v], f2{kLog2e, kLog2e}, nml);
       e[v] = f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
     }
     // den = ((0 + e0) + e1 + ...), num = fma(s, e, num) from 0: e0 + 0 == e0 and
     // fma(s0, e0, 0) == s0 * e0 exactly, so the first terms start the chains
-    const f2 den = ((e[0] + e[1]) + e[2]) + e[3];
-    const f2 num = pk_fma(s[3], e[3], pk_fma(s[2], e[2], pk_fma(s[1], e[1], s[0] * e[0])));
+    f2 den = e[0], num = s[0] * e[0];
+#pragma unroll
+    for (int v = 1; v < NV; ++v) {
+      den = den + e[v];
+      num = pk_fma(s[v], e[v], num);
+    }
     return num * f2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
   }
 }
@@ -360,18 +370,27 @@ struct Region {
 // select is not folded into an indexed load from a stack copy of the array.)
 __device__ __forceinline__ int rfl(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
-__device__ __forceinline__ Region pick_region(const Region (&rg)[4], int u) {
+template <int NV>
+__device__ __forceinline__ Region pick_region(const Region (&rg)[NV], int u) {
   Region r;
+  if constexpr (NV == 4) {
 #define MVN_PICK(f) r.f = u == 0 ? rfl(rg[0].f) : u == 1 ? rfl(rg[1].f) : u == 2 ? rfl(rg[2].f) : rfl(rg[3].f)
-  MVN_PICK(x0); MVN_PICK(y0); MVN_PICK(bw); MVN_PICK(bh); MVN_PICK(pitch); MVN_PICK(sbase); MVN_PICK(xa);
-  MVN_PICK(cw); MVN_PICK(cbase); MVN_PICK(pass); MVN_PICK(cend); MVN_PICK(inv_cw);
+    MVN_PICK(x0); MVN_PICK(y0); MVN_PICK(bw); MVN_PICK(bh); MVN_PICK(pitch); MVN_PICK(sbase); MVN_PICK(xa);
+    MVN_PICK(cw); MVN_PICK(cbase); MVN_PICK(pass); MVN_PICK(cend); MVN_PICK(inv_cw);
 #undef MVN_PICK
+  } else {
+#define MVN_PICK(f)                                                   \
+  r.f = rfl(rg[0].f);                                                 \
+  _Pragma("unroll") for (int k = 1; k < NV; ++k) r.f = u == k ? rfl(rg[k].f) : r.f
+    MVN_PICK(x0); MVN_PICK(y0); MVN_PICK(bw); MVN_PICK(bh); MVN_PICK(pitch); MVN_PICK(sbase); MVN_PICK(xa);
+    MVN_PICK(cw); MVN_PICK(cbase); MVN_PICK(pass); MVN_PICK(cend); MVN_PICK(inv_cw);
+#undef MVN_PICK
+  }
   return r;
 }
 
-
-// The four-view kernel (unproject_x4.hip): MVN_OK, an error code, or 1 when it does not
-// apply to the call (then launch_tiled runs the generic kernel).
+// The chunk-staged kernel for 4 and 8 views (unproject_x4.hip): MVN_OK, an error code, or 1
+// when it does not apply to the call (then launch_tiled runs the generic kernel).
 template <int AGG, typename TIn, typename TOut>
 int launch_x4(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
               const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,

@@ -26,10 +26,11 @@ def time_it(fn, iters):
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     dev = torch.device("cuda:0")
-    for B, dt, label in ((8, torch.float32, "cfg2 f32 B=8"), (32, torch.bfloat16, "cfg3 bf16 B=32")):
-        vb = synth.volumetric_batch(B, dtype=dt, device=dev, seed=0)
+    for B, N, dt, label in ((8, 4, torch.float32, "cfg2 f32 B=8"), (32, 4, torch.bfloat16, "cfg3 bf16 B=32"),
+                            (16, 8, torch.float32, "cfg4 8v f32 B=16")):
+        vb = synth.volumetric_batch(B, n_views=N, dtype=dt, device=dev, seed=0)
         E = 2 if dt == torch.bfloat16 else 4
-        nbytes = B * (E * (4 * 32 * 96 * 96 + 32 * 64 ** 3) + 12 * 64 ** 3 + 4 * 48)
+        nbytes = B * (E * (N * 32 * 96 * 96 + 32 * 64 ** 3) + 12 * 64 ** 3 + 4 * 12 * N)
         res, outs = {}, {}
         for rnd in range(3):
             for kern, generic in (("x4", False), ("tiled", True)):

@@ -15,28 +15,45 @@
 //           the normalised volume (skipped when the caller does not want it).
 #include "common.hpp"
 
+// The finalize is the volume's last reader and its output is written once: both streams
+// non-temporal, so that they do not evict what the next launches read from the MALL (the
+// unprojection's feature maps and coordinates: bench step 292 -> 261 us at config 2).
+#ifndef MVN_SA_NT
+#define MVN_SA_NT 2      // A/B: 0 = plain, 1 = non-temporal stores only, 2 = stores and loads
+#endif
+
 namespace mvn {
 namespace {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
 
 constexpr int kSaBlock = 256;
 constexpr int kSaVpt = 16;                      // voxels per thread
 constexpr int kSaChunk = kSaBlock * kSaVpt;     // 4096 voxels per block
 constexpr int kPartial = 5;                     // m, s, sx, sy, sz
-constexpr int kPartChunk = 512;                 // voxels per pass-1 wave (all joints)
+#ifndef MVN_SA_PCHUNK_F32
+#define MVN_SA_PCHUNK_F32 512
+#endif
+// voxels per pass-1 wave (all joints), per volume dtype; the workspace is sized for the smaller
+template <typename T> constexpr int kPartChunkT = sizeof(T) == 4 ? MVN_SA_PCHUNK_F32 : 512;
+constexpr int kPartChunkMin = MVN_SA_PCHUNK_F32 < 512 ? MVN_SA_PCHUNK_F32 : 512;
 
 template <typename T> struct Vec;
 template <> struct Vec<float> { static constexpr int n = 4; };
 template <> struct Vec<uint16_t> { static constexpr int n = 8; };
 
 // Load `n` consecutive elements starting at i (vector load when fully in range).
-template <typename T, int n>
+template <typename T, int n, bool NT = false>
 __device__ __forceinline__ void load_run(const T* __restrict__ p, int i, int nvox, bool vec_ok, float (&v)[n], float fill) {
   if (vec_ok && i + n <= nvox) {
     if constexpr (sizeof(T) == 4) {
-      const float4 q = *reinterpret_cast<const float4*>(p + i);
+      const f4v q = NT ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p + i))
+                       : *reinterpret_cast<const f4v*>(p + i);
       v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
     } else {
-      const uint4 q = *reinterpret_cast<const uint4*>(p + i);
+      const u4v q = NT ? __builtin_nontemporal_load(reinterpret_cast<const u4v*>(p + i))
+                       : *reinterpret_cast<const u4v*>(p + i);
       const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -50,16 +67,19 @@ __device__ __forceinline__ void load_run(const T* __restrict__ p, int i, int nvo
   }
 }
 
-template <typename T, int n>
+template <typename T, int n, bool NT = false>
 __device__ __forceinline__ void store_run(T* __restrict__ p, int i, int nvox, bool vec_ok, const float (&v)[n]) {
   if (vec_ok && i + n <= nvox) {
     if constexpr (sizeof(T) == 4) {
-      *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);
+      const f4v q = {v[0], v[1], v[2], v[3]};
+      if (NT) __builtin_nontemporal_store(q, reinterpret_cast<f4v*>(p + i));
+      else *reinterpret_cast<f4v*>(p + i) = q;
     } else {
-      uint32_t w[4];
+      u4v q;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) w[k] = pack_bf16x2(v[2 * k], v[2 * k + 1]);
-      *reinterpret_cast<uint4*>(p + i) = make_uint4(w[0], w[1], w[2], w[3]);
+      for (int k = 0; k < 4; ++k) q[k] = pack_bf16x2(v[2 * k], v[2 * k + 1]);
+      if (NT) __builtin_nontemporal_store(q, reinterpret_cast<u4v*>(p + i));
+      else *reinterpret_cast<u4v*>(p + i) = q;
     }
   } else {
 #pragma unroll
@@ -127,6 +147,7 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     const float* __restrict__ cub, int V, int transfer, float mult, float* __restrict__ part, int J, int nvox,
     int nchunk, bool vec_ok) {
   constexpr int VEC = Vec<T>::n;
+  constexpr int kPartChunk = kPartChunkT<T>;
   constexpr int RUNS = kPartChunk / (kWave * VEC);
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const int chunk = blockIdx.x * (kSaBlock / kWave) + wid, b = blockIdx.y;
@@ -318,7 +339,7 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_finalize(
   float t[RUNS][VEC];
 #pragma unroll
   for (int r = 0; r < RUNS; ++r)
-    load_run<T, VEC>(vj, chunk * kSaChunk + r * kSaBlock * VEC + tid * VEC, nvox, vec_ok, t[r], 0.f);
+    load_run<T, VEC, (MVN_SA_NT >= 2)>(vj, chunk * kSaChunk + r * kSaBlock * VEC + tid * VEC, nvox, vec_ok, t[r], 0.f);
 #pragma unroll
   for (int r = 0; r < RUNS; ++r) {
     const int i = chunk * kSaChunk + r * kSaBlock * VEC + tid * VEC;
@@ -329,13 +350,13 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_finalize(
       y[k] = SOFTMAX ? __expf(v - m) * inv : fmaxf(v, 0.f);
     }
     if constexpr (sizeof(TO) == sizeof(T)) {
-      store_run<TO, VEC>(oj, i, nvox, vec_ok, y);
+      store_run<TO, VEC, (MVN_SA_NT >= 1)>(oj, i, nvox, vec_ok, y);
     } else {  // bf16 in -> f32 out: two float4 runs
       float lo[4] = {y[0], y[1], y[2], y[3]};
-      store_run<TO, 4>(oj, i, nvox, vec_ok, lo);
+      store_run<TO, 4, (MVN_SA_NT >= 1)>(oj, i, nvox, vec_ok, lo);
       if constexpr (VEC == 8) {
         float hi[4] = {y[4], y[5], y[6], y[7]};
-        store_run<TO, 4>(oj, i + 4, nvox, vec_ok, hi);
+        store_run<TO, 4, (MVN_SA_NT >= 1)>(oj, i + 4, nvox, vec_ok, hi);
       }
     }
   }
@@ -345,7 +366,7 @@ template <typename T, typename TO, bool SOFTMAX>
 int launch(const void* vol, long long bs, long long js, const float* coords, const float* cub, int V, int transfer,
            float mult, float* xyz, void* out, float* part, int B, int J, int nvox, hipStream_t st) {
   const int nchunk = (nvox + kSaChunk - 1) / kSaChunk;       // pass-2 blocks per (b, j)
-  const int npart = (nvox + kPartChunk - 1) / kPartChunk;     // pass-1 partials per (b, j)
+  const int npart = (nvox + kPartChunkT<T> - 1) / kPartChunkT<T>;   // pass-1 partials per (b, j)
   const bool vec_ok = (reinterpret_cast<uintptr_t>(vol) % 16 == 0) && (bs * sizeof(T)) % 16 == 0 &&
                       (js * sizeof(T)) % 16 == 0 && (nvox % 8 == 0) &&
                       (out == nullptr || reinterpret_cast<uintptr_t>(out) % 16 == 0);
@@ -381,7 +402,7 @@ int softargmax_entry(const void* vol, int vol_dtype, int64_t vol_bstride, int64_
 extern "C" size_t mvn_softargmax3d_workspace_bytes(int B, int J, int Vx, int Vy, int Vz) {
   if (B <= 0 || J <= 0 || Vx <= 0 || Vy <= 0 || Vz <= 0) return 0;
   const long long nvox = (long long)Vx * Vy * Vz;
-  const long long npart = (nvox + mvn::kPartChunk - 1) / mvn::kPartChunk;
+  const long long npart = (nvox + mvn::kPartChunkMin - 1) / mvn::kPartChunkMin;
   return size_t(B) * J * (npart * mvn::kPartial + 2) * sizeof(float);   // partials + (max, 1/sum)
 }
 

@@ -350,12 +350,15 @@ __device__ __forceinline__ f2 aggregate_pair(const f2 (&s)[NV], const f2 (&cf)[N
   }
 }
 
+#ifndef MVN_X4_STORE_POLICY
+#define MVN_X4_STORE_POLICY 0   // A/B: cache policy bits of the output stores (2 = nt)
+#endif
 template <typename T> __device__ __forceinline__ void store_plane(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
 template <> __device__ __forceinline__ void store_plane<float>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, MVN_X4_STORE_POLICY);
 }
 template <> __device__ __forceinline__ void store_plane<uint16_t>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
-  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, 0);
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, MVN_X4_STORE_POLICY);
 }
 
 // Per-view region of the LDS image (block-uniform, SGPRs).

@@ -1,0 +1,84 @@
+"""A/B of the whole bench step (unproject softmax -> soft-argmax over channels [0:17]) across
+builds of libmvn_hip.so, interleaved in one process, so that cache effects between the two
+launches (what one leaves in the MALL for the next) are part of the measurement.
+    python tools/ab_step.py libA.so libB.so ... [--steps K]"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "learnable-triangulation-pytorch_amd"))
+import torch  # noqa: E402
+
+from mvn_rocm import _lib, synth  # noqa: E402
+
+
+def load(path):
+    lib = ctypes.CDLL(os.path.abspath(path))
+    for n in ("mvn_unproject", "mvn_softargmax3d", "mvn_softargmax3d_workspace_bytes"):
+        res, args = _lib.SIGNATURES[n]
+        getattr(lib, n).restype, getattr(lib, n).argtypes = res, args
+    return lib
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    steps = 20
+    libs = [(os.path.basename(p), load(p)) for p in args]
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    for B, dt, label in ((8, torch.float32, "cfg2 f32 B=8"), (32, torch.bfloat16, "cfg3 bf16 B=32")):
+        vb = synth.volumetric_batch(B, dtype=dt, device=dev, seed=0)
+        code = 1 if dt == torch.bfloat16 else 0
+        V3 = 64 ** 3
+        vol = torch.empty((B, 32, 64, 64, 64), dtype=dt, device=dev)
+        xyz = torch.empty((B, 17, 3), device=dev)
+        vout = torch.empty((B, 17, 64, 64, 64), dtype=dt, device=dev)
+        res, ref = {}, {}
+        for rnd in range(3):
+            for name, lib in libs:
+                ws = torch.empty(lib.mvn_softargmax3d_workspace_bytes(B, 17, 64, 64, 64), dtype=torch.uint8, device=dev)
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
+                def step(mark):
+                    if mark:
+                        ev[0].record()
+                    r = lib.mvn_unproject(vb.features.data_ptr(), code, vb.proj.data_ptr(), vb.coords.data_ptr(), None,
+                                          vol.data_ptr(), code, B, 4, 32, 96, 96, 64, 64, 64, 2, 0, st)
+                    assert r == 0, r
+                    if mark:
+                        ev[1].record()
+                    r = lib.mvn_softargmax3d(vol.data_ptr(), code, 32 * V3, V3, vb.coords.data_ptr(), 1.0, 1,
+                                             xyz.data_ptr(), vout.data_ptr(), code, ws.data_ptr(), ws.numel(),
+                                             B, 17, 64, 64, 64, st)
+                    assert r == 0, r
+                    if mark:
+                        ev[2].record()
+                for _ in range(5):
+                    step(False)
+                torch.cuda.synchronize()
+                un = sa = 0.0
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record()
+                for _ in range(steps):
+                    step(True)
+                    torch.cuda.synchronize()
+                    un += ev[0].elapsed_time(ev[1])
+                    sa += ev[1].elapsed_time(ev[2])
+                t1.record()
+                torch.cuda.synchronize()
+                res.setdefault(name, []).append((un / steps, sa / steps))
+                if rnd == 0:
+                    ref[name] = (xyz.clone(), vout.clone())
+        base = libs[0][0]
+        for name, v in res.items():
+            un = min(a for a, _ in v)
+            sa = min(b for _, b in v)
+            same = torch.equal(ref[name][0], ref[base][0]) and torch.equal(ref[name][1], ref[base][1])
+            print(f"{label:16s} {name:14s} unproject {un * 1e3:7.1f} us  softargmax {sa * 1e3:7.1f} us  "
+                  f"step {(un + sa) * 1e3:7.1f} us  -> {B / (un + sa) * 1e3:8.0f} frames/s  same-as-{base}: {same}",
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -350,12 +350,18 @@ __device__ __forceinline__ f2 aggregate_pair(const f2 (&s)[NV], const f2 (&cf)[N
   }
 }
 
+// Cache policy of the four-view kernel's NCDHW output stores (2 = nt).  f32 planes stream
+// out non-temporally so that they do not evict the feature maps the next tiles re-read
+// (whole step at config 2: 261.5 -> 257.8 us); 2-byte bf16 stores must not (577 -> 1,664 us).
 #ifndef MVN_X4_STORE_POLICY
-#define MVN_X4_STORE_POLICY 0   // A/B: cache policy bits of the output stores (2 = nt)
+#define MVN_X4_STORE_POLICY 0
+#endif
+#ifndef MVN_X4_STORE_POLICY_F32
+#define MVN_X4_STORE_POLICY_F32 2
 #endif
 template <typename T> __device__ __forceinline__ void store_plane(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
 template <> __device__ __forceinline__ void store_plane<float>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, MVN_X4_STORE_POLICY);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, MVN_X4_STORE_POLICY_F32);
 }
 template <> __device__ __forceinline__ void store_plane<uint16_t>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
   __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, MVN_X4_STORE_POLICY);

@@ -122,7 +122,31 @@ class Clock:
         return float(t.item())
 
 
+def settle_steps(step, args, clock):
+    """Untimed clock settling before the warmup: the GPU comes out of idle (process start,
+    host-side data generation) at a low clock and takes ~25 ms of back-to-back launches to
+    reach its loaded clock (config-2 unprojection 214 -> 172 us over the first 90 steps,
+    tools/warmup_curve.py; MI355X_MICROARCH.md 'DVFS give-back' measures after >= 2 s of
+    launches).  Runs ~args.settle seconds of steps, the same count on every rank (a step
+    may hold a collective)."""
+    if args.settle <= 0 or clock.dry:
+        return 0
+    for _ in range(3):          # first launches (code loading) are not representative
+        step(False)
+    clock.sync()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        step(False)
+    clock.sync()
+    per = max((time.perf_counter() - t0) / 5, 1e-5)
+    n = int(clock.max_over_ranks(min(args.settle / per, 100000.0)))
+    for _ in range(n):
+        step(False)
+    return n + 8
+
+
 def timed_loop(step, args, clock):
+    settle_steps(step, args, clock)
     for _ in range(args.warmup):
         step(False)
     clock.fence()
@@ -424,8 +448,10 @@ def dry_run(args, rank, world):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--settle", type=float, default=1.0,
+                    help="seconds of untimed steps before the warmup, per config (GPU clock ramp from idle)")
     ap.add_argument("--config", default="2", choices=["2", "3", "4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
@@ -514,6 +540,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_s": args.settle,
             "ms_per_step": r["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",

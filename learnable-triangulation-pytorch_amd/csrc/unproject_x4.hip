@@ -73,6 +73,9 @@ __device__ unsigned long long g_x4_stamps[1 << 21];
 #ifndef MVN_X4_CORNER
 #define MVN_X4_CORNER 0  // 1: footprint boxes from the tile's corners (no barrier), else exact per voxel
 #endif
+#ifndef MVN_X4_XCD_MIN_FRAMES
+#define MVN_X4_XCD_MIN_FRAMES 1    // from this many frames each XCD takes the same slab of every frame
+#endif
 #ifndef MVN_X4_ROWINT
 #define MVN_X4_ROWINT 0  // 1: chunks numbered over groups of 4 rows (conflict-free ds_write_b128)
 #endif
@@ -121,7 +124,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   int L = int(blockIdx.x);
   {
     const int nf = nTx * nTy * nTz;
-    if (B >= 16 && nf % 8 == 0) {
+    if (B >= MVN_X4_XCD_MIN_FRAMES && nf % 8 == 0) {
       const int xcd = int(blockIdx.x) % 8, k = int(blockIdx.x) / 8, slab = nf / 8;
       L = (k / slab) * nf + xcd * slab + k % slab;
     }

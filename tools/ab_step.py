@@ -24,11 +24,15 @@ def load(path):
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     steps = 20
+    sync_each = "--sync" in sys.argv      # default: steps back to back, as bench.py runs them
     libs = [(os.path.basename(p), load(p)) for p in args]
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
-    for B, dt, label in ((8, torch.float32, "cfg2 f32 B=8"), (32, torch.bfloat16, "cfg3 bf16 B=32")):
-        vb = synth.volumetric_batch(B, dtype=dt, device=dev, seed=0)
+    for B, N, dt, label in ((8, 4, torch.float32, "cfg2 f32 B=8"), (32, 4, torch.bfloat16, "cfg3 bf16 B=32"),
+                            (16, 8, torch.float32, "cfg4 8v B=16"), (128, 8, torch.float32, "cfg4 8v B=128")):
+        if "--no8" in sys.argv and N == 8:
+            continue
+        vb = synth.volumetric_batch(B, n_views=N, dtype=dt, device=dev, seed=0)
         code = 1 if dt == torch.bfloat16 else 0
         V3 = 64 ** 3
         vol = torch.empty((B, 32, 64, 64, 64), dtype=dt, device=dev)
@@ -38,13 +42,14 @@ def main():
         for rnd in range(3):
             for name, lib in libs:
                 ws = torch.empty(lib.mvn_softargmax3d_workspace_bytes(B, 17, 64, 64, 64), dtype=torch.uint8, device=dev)
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                evs = []
 
                 def step(mark):
+                    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if mark else None
                     if mark:
                         ev[0].record()
                     r = lib.mvn_unproject(vb.features.data_ptr(), code, vb.proj.data_ptr(), vb.coords.data_ptr(), None,
-                                          vol.data_ptr(), code, B, 4, 32, 96, 96, 64, 64, 64, 2, 0, st)
+                                          vol.data_ptr(), code, B, N, 32, 96, 96, 64, 64, 64, 2, 0, st)
                     assert r == 0, r
                     if mark:
                         ev[1].record()
@@ -54,19 +59,17 @@ def main():
                     assert r == 0, r
                     if mark:
                         ev[2].record()
+                        evs.append(ev)
                 for _ in range(5):
                     step(False)
                 torch.cuda.synchronize()
-                un = sa = 0.0
-                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                t0.record()
                 for _ in range(steps):
                     step(True)
-                    torch.cuda.synchronize()
-                    un += ev[0].elapsed_time(ev[1])
-                    sa += ev[1].elapsed_time(ev[2])
-                t1.record()
+                    if sync_each:
+                        torch.cuda.synchronize()
                 torch.cuda.synchronize()
+                un = sum(e[0].elapsed_time(e[1]) for e in evs)
+                sa = sum(e[1].elapsed_time(e[2]) for e in evs)
                 res.setdefault(name, []).append((un / steps, sa / steps))
                 if rnd == 0:
                     ref[name] = (xyz.clone(), vout.clone())

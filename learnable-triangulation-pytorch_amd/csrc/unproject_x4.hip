@@ -76,6 +76,12 @@ __device__ unsigned long long g_x4_stamps[1 << 21];
 #ifndef MVN_X4_XCD_MIN_FRAMES
 #define MVN_X4_XCD_MIN_FRAMES 1    // from this many frames each XCD takes the same slab of every frame
 #endif
+#ifndef MVN_X4_LDS_STORE
+#define MVN_X4_LDS_STORE 1          // bf16 NCDHW output: rows of TZ voxels gathered in LDS, 16-byte stores
+#endif
+#ifndef MVN_X4_LDS_STORE_POLICY
+#define MVN_X4_LDS_STORE_POLICY 0   // cache policy of those 16-byte stores (2 = nt)
+#endif
 #ifndef MVN_X4_ROWINT
 #define MVN_X4_ROWINT 0  // 1: chunks numbered over groups of 4 rows (conflict-free ds_write_b128)
 #endif
@@ -118,6 +124,11 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
 
   __shared__ uint4 stage[2 * kBuf];
   __shared__ int red[kWaves][NV][4];
+  // bf16 NCDHW output: each group's G channel planes of the tile gathered in LDS (double
+  // buffered), then stored as 16-byte rows (TZ = 8 voxels) one barrier later — instead of
+  // one 2-byte store per voxel and channel
+  constexpr bool kLdsOut = MVN_X4_LDS_STORE && sizeof(TOut) == 2 && TZ * sizeof(TOut) == 16;
+  __shared__ uint16_t ost[kLdsOut ? 2 * G * kThreads : 1];
 
   // ---- which tile (z-tiles fastest; block order as unproject_tiled) ------------------
   const int nTx = (Vx + TX - 1) / TX, nTy = (Vy + TY - 1) / TY, nTz = (Vz + TZ - 1) / TZ;
@@ -307,6 +318,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   const __amdgpu_buffer_rsrc_t frs = make_rsrc(fb, uint32_t(size_t(NV) * C * HW * E));
   const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + size_t(b) * C * nvox, uint32_t(size_t(C) * nvox * sizeof(TOut)));
   const uint32_t ooff = act ? uint32_t(vox) * uint32_t(sizeof(TOut)) : kOob;
+  const bool lds_out = kLdsOut && !out_cl && (X0 + TX <= Vx) && (Y0 + TY <= Vy) && (Z0 + TZ <= Vz);
   const uint32_t ooff_cl = act ? uint32_t(vox) * uint32_t(C) * uint32_t(sizeof(TOut)) : kOob;
 
   // LDS byte offsets of each view's north-west and south-west taps; a voxel whose base
@@ -411,7 +423,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight
     }
   };
-  auto aggregate_store = [&](int c0, const f2 (&sv)[2][NV]) __attribute__((always_inline)) {
+  auto aggregate_store = [&](int c0, const f2 (&sv)[2][NV], bool to_lds) __attribute__((always_inline)) {
     float r[G];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -439,16 +451,36 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
             ors, ooff_cl, soff, 0);
       return;
     }
+    if (kLdsOut && to_lds) {
+      uint16_t* o = ost + ((c0 / G) & 1) * (G * kThreads) + t;
+#pragma unroll
+      for (int ch = 0; ch < G; ++ch) o[ch * kThreads] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r[ch]));
+      return;
+    }
 #pragma unroll
     for (int ch = 0; ch < G; ++ch)
       if (!MVN_X4_ABL_NOSTORE || r[ch] == 1234.5f)
         store_plane<TOut>(r[ch], ors, ooff, uint32_t(c0 + ch) * uint32_t(nvox) * uint32_t(sizeof(TOut)));
   };
+  // the 16-byte rows of group c0 (after the barrier that follows its consume)
+  auto flush = [&](int c0) __attribute__((always_inline)) {
+    if constexpr (kLdsOut) {
+      constexpr int kRows = G * TX * TY;                      // one row = TZ voxels of one channel
+      if (!lds_out || t >= kRows) return;
+      const int ch = t / (TX * TY), row = t - ch * (TX * TY);
+      const uint4 q = *reinterpret_cast<const uint4*>(ost + ((c0 / G) & 1) * (G * kThreads) + ch * kThreads + row * TZ);
+      const int x = row / TY, y = row - x * TY;
+      const uint32_t voff = uint32_t(((X0 + x) * Vy + (Y0 + y)) * Vz + Z0) * uint32_t(sizeof(TOut));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, q),
+                                             ors, voff, uint32_t(c0 + ch) * uint32_t(nvox) * uint32_t(sizeof(TOut)),
+                                             MVN_X4_LDS_STORE_POLICY);
+    }
+  };
 
   auto consume = [&](const uint4* buf, int c0) __attribute__((always_inline)) {
     f2 sv[2][NV];
     sample_views(reinterpret_cast<const char*>(buf), true, 0, sv);
-    aggregate_store(c0, sv);
+    aggregate_store(c0, sv, lds_out);         // (single-pass loop: rows flushed after the barrier)
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -489,26 +521,33 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     __syncthreads();
     X4_STAMP(6);
     X4_ACC_DECL;
+    int last = 0;
     for (int c0 = 0; c0 < C; c0 += 2 * G) {
       const bool more1 = c0 + G < C, more2 = c0 + 2 * G < C;
       if (more1) issue(c0 + G);
       X4_ACC(3);
       consume(stage, c0);
       X4_ACC(0);
-      if (!more1) break;
+      if (!more1) { last = c0; break; }
       commit(stage + kBuf);
       X4_ACC(1);
       __syncthreads();
+      flush(c0);
       X4_ACC(2);
       if (more2) issue(c0 + 2 * G);
       X4_ACC(3);
       consume(stage + kBuf, c0 + G);
       X4_ACC(0);
-      if (!more2) break;
+      if (!more2) { last = c0 + G; break; }
       commit(stage);
       X4_ACC(1);
       __syncthreads();
+      flush(c0 + G);
       X4_ACC(2);
+    }
+    if (kLdsOut && lds_out) {                 // the last group's rows
+      __syncthreads();
+      flush(last);
     }
     X4_STAMP(7);
     X4_ACC_STORE;
@@ -538,7 +577,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       sample_views(reinterpret_cast<const char*>(stage), false, pass, sv);
       __syncthreads();
     }
-    aggregate_store(c0, sv);
+    aggregate_store(c0, sv, false);
   }
   fix_voxel();
 }

@@ -106,6 +106,51 @@ template <> struct X4Shape<2> {
   static constexpr int TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = MVN_X4_T2_SLOTS, MC = 2, WAVES = MVN_X4_T2_WAVES;
 };
 
+#ifndef MVN_X4_PACKED_REGIONS
+#define MVN_X4_PACKED_REGIONS 1
+#endif
+// Per-view LDS regions (block-uniform, scalar registers).  Unpacked: 12 SGPRs per view (48
+// for 4 views, which spilled to VGPR lanes: ~60 v_writelane / v_readlane in the prologue);
+// packed: 3 words per view — (x0 + 1, y0 + 1), (bw, bh), sbase | cbase << 13 | pass << 24 —
+// and the derived fields recomputed on use.
+__device__ __forceinline__ Region make_region(int x0, int y0, int bw, int bh, int sbase, int cbase, int pass) {
+  Region r;
+  r.x0 = x0; r.y0 = y0; r.bw = bw; r.bh = bh; r.sbase = sbase; r.cbase = cbase; r.pass = pass;
+  r.pitch = bw | 1;                                          // odd: spreads rows over banks
+  r.xa = x0 & ~3;                                            // chunk origin, x % 4 == 0
+  r.cw = bw ? (x0 + bw - r.xa + 3) >> 2 : 0;                 // chunks per row
+  // chunks are numbered over groups of 4 rows, rows fastest (see chunk_fields): rows padded
+  // to a multiple of 4
+  r.cend = cbase + r.cw * (MVN_X4_ROWINT ? (bh + 3) & ~3 : bh);
+  r.inv_cw = r.cw ? __builtin_amdgcn_rcpf(float(r.cw)) : 0.f;
+  return r;
+}
+template <bool PACKED> struct RegionSet {
+  Region rg[4];
+  __device__ __forceinline__ void set(int v, const Region& r) { rg[v] = r; }
+  __device__ __forceinline__ Region get(int v) const { return rg[v]; }
+  __device__ __forceinline__ Region pick(int u) const { return pick_region(rg, u); }
+};
+template <> struct RegionSet<true> {
+  uint32_t a[4], b[4], c[4];
+  __device__ __forceinline__ void set(int v, const Region& r) {
+    a[v] = uint32_t(r.x0 + 1) | (uint32_t(r.y0 + 1) << 16);
+    b[v] = uint32_t(r.bw) | (uint32_t(r.bh) << 16);
+    c[v] = uint32_t(r.sbase) | (uint32_t(r.cbase) << 13) | (uint32_t(r.pass) << 24);
+  }
+  __device__ __forceinline__ static Region unpack(uint32_t a, uint32_t b, uint32_t c) {
+    return make_region(int(a & 0xffffu) - 1, int(a >> 16) - 1, int(b & 0xffffu), int(b >> 16), int(c & 0x1fffu),
+                       int((c >> 13) & 0x7ffu), int(c >> 24));
+  }
+  __device__ __forceinline__ Region get(int v) const { return unpack(a[v], b[v], c[v]); }
+  __device__ __forceinline__ Region pick(int u) const {
+    const uint32_t pa = u == 0 ? rfl(int(a[0])) : u == 1 ? rfl(int(a[1])) : u == 2 ? rfl(int(a[2])) : rfl(int(a[3]));
+    const uint32_t pb = u == 0 ? rfl(int(b[0])) : u == 1 ? rfl(int(b[1])) : u == 2 ? rfl(int(b[2])) : rfl(int(b[3]));
+    const uint32_t pc = u == 0 ? rfl(int(c[0])) : u == 1 ? rfl(int(c[1])) : u == 2 ? rfl(int(c[2])) : rfl(int(c[3]));
+    return unpack(pa, pb, pc);
+  }
+};
+
 template <int AGG, typename TIn, typename TOut, int K>
 __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_per_eu(X4Shape<K>::WAVES))) void unproject_x4(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
@@ -247,34 +292,64 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       box[v][3] = min(int(floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cbox[3]), 8 * v)))), H - 1);
     }
   } else {
-    // exact: every voxel's base pixel, DPP min / max per wave, combined over the waves
+    // exact: every voxel's base pixel.  The 16 per-wave reductions (4 views x min x0, max x1,
+    // min y0, max y1; maxima as minima of negated values) run as one transposing butterfly:
+    // lanes 32 apart swap halves of their 16 values (v_permlane32_swap), then rows 16 apart
+    // (v_permlane16_swap), then lanes 8 and "4" apart (DPP row_ror:8, row_half_mirror) each
+    // keep one of two, and the quads reduce — 35 instructions instead of 16 DPP reductions
+    // with their readlanes.  Lane l ends with value (l >> 2) & 15 of the whole wave.
+    int q16[16];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const int x0 = wave_min_u(has[v] ? fx[v] : INT_MAX), x1 = wave_max_u(has[v] ? fx[v] : INT_MIN);
-      const int y0 = wave_min_u(has[v] ? fy[v] : INT_MAX), y1 = wave_max_u(has[v] ? fy[v] : INT_MIN);
-      if (lane == 0) { red[wid][v][0] = x0; red[wid][v][1] = x1; red[wid][v][2] = y0; red[wid][v][3] = y1; }
+      q16[4 * v + 0] = has[v] ? fx[v] : INT_MAX;
+      q16[4 * v + 1] = has[v] ? -fx[v] : INT_MAX;
+      q16[4 * v + 2] = has[v] ? fy[v] : INT_MAX;
+      q16[4 * v + 3] = has[v] ? -fy[v] : INT_MAX;
     }
-    __syncthreads();
-    int part;
-    {
-      const int v = (lane >> 2) & (NV - 1), k = lane & 3;
-      const bool mn = (k & 1) == 0;                           // components: x0 min, x1 max, y0 min, y1 max
-      part = mn ? INT_MAX : INT_MIN;
+    int q8[8], q4[4], q2[2];
 #pragma unroll
-      for (int q = 0; q < kWaves; ++q) {
-        const int r = red[q][v][k];
-        part = mn ? min(part, r) : max(part, r);
-      }
+    for (int i = 0; i < 8; ++i) {
+      const auto r = __builtin_amdgcn_permlane32_swap(unsigned(q16[i]), unsigned(q16[8 + i]), false, false);
+      q8[i] = min(int(r[0]), int(r[1]));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane16_swap(unsigned(q8[i]), unsigned(q8[4 + i]), false, false);
+      q4[i] = min(int(r[0]), int(r[1]));
+    }
+    const bool b3 = lane & 8, b2 = lane & 4;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int send = b3 ? q4[m] : q4[m + 2], keep = b3 ? q4[m + 2] : q4[m];
+      q2[m] = min(keep, __builtin_amdgcn_update_dpp(INT_MAX, send, 0x128, 0xf, 0xf, false));   // row_ror:8
+    }
+    int q1;
+    {
+      const int send = b2 ? q2[0] : q2[1], keep = b2 ? q2[1] : q2[0];
+      q1 = min(keep, __builtin_amdgcn_update_dpp(INT_MAX, send, 0x141, 0xf, 0xf, false));     // row_half_mirror
+    }
+    q1 = min(q1, __builtin_amdgcn_update_dpp(INT_MAX, q1, 0xb1, 0xf, 0xf, false));              // quad_perm 1,0,3,2
+    q1 = min(q1, __builtin_amdgcn_update_dpp(INT_MAX, q1, 0x4e, 0xf, 0xf, false));              // quad_perm 2,3,0,1
+    if ((lane & 3) == 0) (&red[wid][0][0])[(lane >> 2) & 15] = q1;
+    __syncthreads();
+    int part = INT_MAX;
+    {
+      const int idx = lane & 15;
+#pragma unroll
+      for (int q = 0; q < kWaves; ++q) part = min(part, (&red[q][0][0])[idx]);
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) box[v][k] = __builtin_amdgcn_readlane(part, 4 * v + k);
+      for (int k = 0; k < 4; ++k) {
+        const int m = __builtin_amdgcn_readlane(part, 4 * v + k);
+        box[v][k] = (k & 1) ? -m : m;
+      }
   }
   X4_STAMP(3);
 
   // ---- LDS regions (slots and chunks), in scalar registers ----------------------------
-  Region rg[NV];
+  RegionSet<MVN_X4_PACKED_REGIONS != 0> rs;
   int npass, total;
   {
     int snext = 0, cnext = 0, pass = 0, chunks0 = 0;
@@ -287,17 +362,11 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       int bw = 0, bh = 0;
       if (x0 <= x1 && y0 <= y1) { bw = x1 - x0 + 2; bh = y1 - y0 + 2; }   // +1 px: east / south taps
       else { x0 = 0; y0 = 0; }
-      const int pitch = bw | 1;                                 // odd: spreads rows over banks
-      const int xa = x0 & ~3;                                   // chunk origin, x % 4 == 0
-      const int cw = bw ? (x0 + bw - xa + 3) >> 2 : 0;          // chunks per row
-      // chunks are numbered over groups of 4 rows, rows fastest (see chunk_fields): rows
-      // padded to a multiple of 4
-      const int area = pitch * bh, nch = cw * (MVN_X4_ROWINT ? (bh + 3) & ~3 : bh);
+      const Region r0 = make_region(x0, y0, bw, bh, 0, 0, 0);
+      const int area = r0.pitch * bh, nch = r0.cend;
       if (area > lim || nch > MC * kThreads) too_big = true;
       if (snext + area > lim || cnext + nch > MC * kThreads) { ++pass; snext = 0; cnext = 0; }
-      rg[v].x0 = x0; rg[v].y0 = y0; rg[v].bw = bw; rg[v].bh = bh; rg[v].pitch = pitch; rg[v].sbase = snext;
-      rg[v].xa = xa; rg[v].cw = cw; rg[v].cbase = cnext; rg[v].pass = pass; rg[v].cend = cnext + nch;
-      rg[v].inv_cw = cw ? __builtin_amdgcn_rcpf(float(cw)) : 0.f;
+      rs.set(v, make_region(x0, y0, bw, bh, snext, cnext, pass));
       snext += area;
       cnext += nch;
       if (pass == 0) chunks0 = cnext;
@@ -329,14 +398,15 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   auto tap_slots = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const int dx = fx[v] - rg[v].x0, dy = fy[v] - rg[v].y0;
+      const Region rv = rs.get(v);
+      const int dx = fx[v] - rv.x0, dy = fy[v] - rv.y0;
       // (exact boxes contain every voxel's base pixel by construction)
-      const bool inbox = !MVN_X4_CORNER || ((dx >= 0) & (dx <= rg[v].bw - 2) & (dy >= 0) & (dy <= rg[v].bh - 2));
+      const bool inbox = !MVN_X4_CORNER || ((dx >= 0) & (dx <= rv.bw - 2) & (dy >= 0) & (dy <= rv.bh - 2));
       if (MVN_X4_CORNER) refix |= has[v] & !inbox;             // (has implies act)
       const bool use = has[v] & inbox;
-      const int slot = rg[v].sbase + dy * rg[v].pitch + dx;
+      const int slot = rv.sbase + dy * rv.pitch + dx;
       anw[v] = uint32_t(use ? slot : kZeroSlot) * kSlotB;
-      asw[v] = uint32_t(use ? slot + rg[v].pitch : kZeroSlot) * kSlotB;
+      asw[v] = uint32_t(use ? slot + rv.pitch : kZeroSlot) * kSlotB;
       if (MVN_X4_ABL_BCAST) {
         anw[v] = __builtin_amdgcn_readfirstlane(anw[v]);
         asw[v] = __builtin_amdgcn_readfirstlane(asw[v]);
@@ -412,7 +482,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   auto sample_views = [&](const char* buf, bool all, int pass, f2 (&sv)[2][NV]) __attribute__((always_inline)) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      if (!all && rg[v].pass != pass) continue;
+      if (!all && rs.get(v).pass != pass) continue;
       const uint4 a = *reinterpret_cast<const uint4*>(buf + anw[v]);
       const uint4 bq = *reinterpret_cast<const uint4*>(buf + anw[v] + kSlotB);
       const uint4 cq = *reinterpret_cast<const uint4*>(buf + asw[v]);
@@ -495,8 +565,8 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       int sel = 0;
 #pragma unroll
       for (int u = 1; u < NV; ++u)
-        if (rg[u].cw > 0 && k >= rg[u].cbase) sel = u;
-      const Region r = pick_region(rg, sel);
+        if (rs.get(u).cw > 0 && k >= rs.get(u).cbase) sel = u;
+      const Region r = rs.pick(sel);
       chunk_fields(r, sel, k - r.cbase, goff[i], s0[i], mask[i], k < total);
     }
     const int wfirst = __builtin_amdgcn_readfirstlane(wid * kWave);
@@ -562,12 +632,13 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     for (int pass = 0; pass < npass; ++pass) {
 #pragma unroll
       for (int v = 0; v < NV; ++v) {          // every thread stages chunks of each view of the pass
-        if (rg[v].pass != pass) continue;
-        const int nch = rg[v].cend - rg[v].cbase;
+        const Region rv = rs.get(v);
+        if (rv.pass != pass) continue;
+        const int nch = rv.cend - rv.cbase;
         for (int li = t; li < nch; li += kThreads) {
           uint32_t goff, mask;
           int s0;
-          chunk_fields(rg[v], v, li, goff, s0, mask, true);
+          chunk_fields(rv, v, li, goff, s0, mask, true);
           Chunk pre[G];
           load_group(pre, goff, c0);
           write_group(stage, pre, s0, mask);
@@ -596,7 +667,7 @@ template <int AGG, typename TIn, typename TOut>
 int launch_x4(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
               const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
               int align_corners, int out_cl, hipStream_t s) {
-  if (N != 4 || W % 4 != 0 || C % 4 != 0) return 1;
+  if (N != 4 || W % 4 != 0 || C % 4 != 0 || H > 32000 || W > 32000) return 1;
   if ((long long)N * C * H * W * sizeof(TIn) >= (1LL << 31) ||
       (long long)C * Vx * Vy * Vz * sizeof(TOut) >= (1LL << 31))
     return MVN_ERR_SHAPE;

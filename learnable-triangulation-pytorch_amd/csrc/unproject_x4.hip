@@ -85,6 +85,9 @@ __device__ unsigned long long g_x4_stamps[1 << 21];
 #ifndef MVN_X4_PATCH_LANES
 #define MVN_X4_PATCH_LANES 1        // lane groups of ds_read_b128 take compact 2 x 8 (y, z) voxel patches
 #endif
+#ifndef MVN_X4_CL_GROUPS
+#define MVN_X4_CL_GROUPS 4          // bf16 channels-last: channel groups per run of 16-byte stores (1, 2, 4)
+#endif
 #ifndef MVN_X4_ROWINT
 #define MVN_X4_ROWINT 0  // 1: chunks numbered over groups of 4 rows (conflict-free ds_write_b128)
 #endif
@@ -514,6 +517,9 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight
     }
   };
+  uint2 cl_buf[MVN_X4_CL_GROUPS > 1 ? MVN_X4_CL_GROUPS - 1 : 1];
+#pragma unroll
+  for (int k = 0; k < (MVN_X4_CL_GROUPS > 1 ? MVN_X4_CL_GROUPS - 1 : 1); ++k) cl_buf[k] = make_uint2(0u, 0u);
   auto aggregate_store = [&](int c0, const f2 (&sv)[2][NV], bool to_lds) __attribute__((always_inline)) {
     float r[G];
 #pragma unroll
@@ -529,6 +535,37 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     }
     if (out_cl) {
       const uint32_t soff = uint32_t(c0) * uint32_t(sizeof(TOut));
+      if constexpr (sizeof(TOut) == 2 && MVN_X4_CL_GROUPS > 1) {
+        // bf16 channels-last: MVN_X4_CL_GROUPS groups' 8-byte pieces of the voxel's record are
+        // held in registers and go out as 16-byte stores of consecutive channels
+        constexpr int NG = MVN_X4_CL_GROUPS;
+        const uint2 cur = make_uint2(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[2], r[3]));
+        const int gi = (c0 / G) % NG;
+        if (gi == NG - 1) {
+#pragma unroll
+          for (int k = 0; k + 1 < NG; k += 2) {
+            const uint2 hi = k + 1 == NG - 1 ? cur : cl_buf[k + 1];
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
+                                   make_uint4(cl_buf[k].x, cl_buf[k].y, hi.x, hi.y)),
+                ors, ooff_cl, soff - uint32_t((NG - 1 - k) * G * sizeof(TOut)), 0);
+          }
+        } else if (c0 + G >= C) {            // C / G not a multiple of NG: the tail group by itself
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, cur),
+                                                ors, ooff_cl, soff, 0);
+#pragma unroll
+          for (int k = 0; k < NG - 1; ++k)
+            if (k < gi)
+              __builtin_amdgcn_raw_buffer_store_b64(
+                  __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, cl_buf[k]), ors, ooff_cl,
+                  soff - uint32_t((gi - k) * G * sizeof(TOut)), 0);
+        } else {
+#pragma unroll
+          for (int k = 0; k < NG - 1; ++k)
+            if (k == gi) cl_buf[k] = cur;
+        }
+        return;
+      }
       if constexpr (sizeof(TOut) == 4)
         __builtin_amdgcn_raw_buffer_store_b128(
             __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,

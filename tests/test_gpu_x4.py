@@ -102,12 +102,14 @@ def test_x4_non_affine_coordinates(device, method):
         np.testing.assert_array_equal(out.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("channels", (32, 12, 20))
 @pytest.mark.parametrize("dt", (torch.float32, torch.bfloat16))
-def test_x4_channels_last_and_cuboids_equal_generic(device, dt):
+def test_x4_channels_last_and_cuboids_equal_generic(device, dt, channels):
     """Channels-last output (config 5) and in-kernel cuboid coordinates through the
-    four-view kernel, bit-identical to the generic kernel."""
+    four-view kernel, bit-identical to the generic kernel (12 / 20 channels: a channel
+    group count that is not a multiple of the bf16 store grouping)."""
     from mvn_rocm import _lib, synth, v2v, volumetric
-    vb = synth.volumetric_batch(2, n_views=4, channels=32, heatmap=96, volume=8, seed=73)
+    vb = synth.volumetric_batch(2, n_views=4, channels=channels, heatmap=96, volume=8, seed=73)
     rng = np.random.default_rng(73)
     base = rng.uniform(-500, 500, (2, 3)) + np.array([0, 0, 900.0])
     cub = volumetric.build_cuboids(base, 2500.0, 32, rng.uniform(0, 2 * np.pi, 2), "coco", False, device=device)

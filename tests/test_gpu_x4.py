@@ -118,3 +118,33 @@ def test_x4_channels_last_and_cuboids_equal_generic(device, dt, channels):
     with _lib.unproject_knobs(generic=True):
         b = v2v.unproject_channels_last(feat, P, cub, "softmax", out_dtype=dt)
     assert torch.equal(_bits(a), _bits(b))
+
+
+@pytest.mark.parametrize("method", METHODS)
+@pytest.mark.parametrize("dt", ("f32", "bf16", "bf16->f32"))
+def test_x4_partial_tiles(device, method, dt):
+    """A volume that is not a multiple of either tile (20 x 28 x 36 of a 40^3 grid): edge
+    tiles with inactive voxels (bf16 output then skips the LDS-gathered rows) next to full
+    ones — bitwise against the generic kernel, and against the oracle."""
+    vb, conf = _batch(device, 74, heatmap=64, volume=40, channels=8)
+    X = vb.coords[:, 2:22, 5:33, 1:37].contiguous()
+    feat = vb.features.to(device)
+    od = None
+    if dt != "f32":
+        feat = feat.to(torch.bfloat16)
+        od = torch.float32 if dt == "bf16->f32" else None
+    P, Xd, cf = vb.proj.to(device), X.to(device), conf.to(device)
+    a = _run(feat, P, Xd, method, cf, od)
+    b = _run(feat, P, Xd, method, cf, od, generic=True)
+    assert a.shape == (2, 8, 20, 28, 36)
+    assert torch.equal(_bits(a), _bits(b))
+    bits = feat.cpu().view(torch.int16).numpy().view(np.uint16) if feat.dtype == torch.bfloat16 else None
+    ref = capi.unproject(bits if bits is not None else vb.features.numpy(), vb.proj.numpy(), X.numpy(),
+                         method, conf.numpy(), feat_bf16_bits=bits is not None)
+    got = a.float().cpu().numpy()
+    if a.dtype == torch.bfloat16:
+        np.testing.assert_allclose(got, ref, rtol=2 ** -8, atol=2 ** -8 * np.abs(ref).max())
+    elif method == "softmax":
+        assert max_rel(got, ref) <= 1e-5
+    else:
+        np.testing.assert_array_equal(got, ref)

@@ -157,6 +157,23 @@ int mvn_v2v_front(const void* vol_cl, const void* weight_packed, const float* sc
                   void* out, int out_dtype, int B, int V, void* stream);
 
 /*
+ * Config 5 in one call: unprojection written channels-last bf16 (as mvn_unproject_ex with
+ * MVN_LAYOUT_NDHWC, or mvn_unproject_cuboid when `cuboids` is given instead of `coords`)
+ * followed by mvn_v2v_front, pipelined over groups of `group_frames` frames (<= 0: the
+ * default, one group's intermediate within half of the 256 MiB MALL: 8 frames at V = 64)
+ * through `workspace` (>= mvn_unproject_v2v_front_workspace_bytes(group_frames, V) bytes).
+ * Replaces triangulation.py:349-352 up to V2VModel.front_layers[0] (v2v.py:145-146).
+ *   C == 32, V % 16 == 0, agg != MVN_AGG_CONF; exactly one of coords / cuboids non-NULL.
+ *   out (B, 16, V, V, V) out_dtype.  Bit-identical to the two calls on the whole batch.
+ */
+size_t mvn_unproject_v2v_front_workspace_bytes(int group_frames, int V);
+int mvn_unproject_v2v_front(const void* feat, int feat_dtype, const float* proj, const float* coords,
+                            const float* cuboids, int transfer_cmu, int agg, int align_corners,
+                            const void* weight_packed, const float* scale, const float* shift, void* out,
+                            int out_dtype, void* workspace, size_t workspace_bytes, int group_frames,
+                            int B, int N, int C, int H, int W, int V, void* stream);
+
+/*
  * 2D soft-argmax of heatmaps.  Replaces mvn/utils/op.py:11-47 (integrate_tensor_2d) with
  * the caller's `heatmaps * heatmap_multiplier` (triangulation.py:164) fused.
  *   heatmaps  (B, J, H, W)  dtype (f32 | bf16), contiguous

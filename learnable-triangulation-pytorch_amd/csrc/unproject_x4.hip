@@ -234,7 +234,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     const Homog hp = homog(Pb + v * 12, o[0], o[1], o[2]);
     const Recip rH0 = recip_refined(float(H)), rW0 = recip_refined(float(W));
     const Proj pc = project_h<false>(hp, H, W, align_corners, rH0, rW0);
-    bool ok = (hp.wh > 0.f) & (fabsf(pc.ix) < 0x1p24f) & (fabsf(pc.iy) < 0x1p24f);
+    bool ok = (hp.wh > 0.f) && (fabsf(pc.ix) < 0x1p24f) && (fabsf(pc.iy) < 0x1p24f);
     cbox[0] = pc.ix - 1e-3f; cbox[1] = pc.ix + 1e-3f; cbox[2] = pc.iy - 1e-3f; cbox[3] = pc.iy + 1e-3f;
 #pragma unroll
     for (int m = 1; m < 8; m <<= 1) {

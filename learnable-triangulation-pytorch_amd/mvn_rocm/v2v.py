@@ -114,3 +114,44 @@ class Basic3DBlockFront(nn.Module):
 
     def forward(self, vol_cl, out_dtype=torch.float32):
         return v2v_front(vol_cl, self.packed, self.scale, self.shift, out_dtype)
+
+
+def unproject_v2v_front(heatmaps, proj_matricies, coord_volumes, packed, scale, shift,
+                        volume_aggregation_method="softmax", out_dtype=torch.float32, group_frames=0,
+                        align_corners=False):
+    """Config 5 in one call (``mvn_unproject_v2v_front``): unproject_heatmaps (op.py:99-163)
+    written channels-last bf16, then the front block relu(bn(conv3d_7)), pipelined over frame
+    groups through a workspace of one group's intermediate (default: 8 frames at V = 64,
+    within half of the MALL).  ``coord_volumes`` may be a ``volumetric.Cuboids``.  Equal to
+    ``v2v_front(unproject_channels_last(...))`` bit for bit."""
+    from .volumetric import Cuboids
+    agg = aggregation_code(volume_aggregation_method)
+    if agg == _lib.MVN_AGG_CONF:
+        raise ValueError("unproject_v2v_front: 'conf*' aggregation is not supported here")
+    cub = coord_volumes if isinstance(coord_volumes, Cuboids) else None
+    feat, proj, _ = unproject_inputs(heatmaps, proj_matricies, None, agg, volume_aggregation_method, cub)
+    fd, od = _dtype_code(feat.dtype), _dtype_code(out_dtype)
+    B, N, C, H, W = feat.shape
+    if C != CIN:
+        raise RuntimeError(f"unproject_v2v_front needs {CIN} heatmap channels, got {C}")
+    if cub is not None:
+        coords, V = None, cub.volume_size
+        _require_gpu(feat, proj, cub.params, packed, scale, shift)
+    else:
+        coords = coord_volumes.float().contiguous()
+        if coords.dim() != 5 or coords.shape[0] != B or coords.shape[4] != 3 or len(set(coords.shape[1:4])) != 1:
+            raise RuntimeError(f"coord_volumes must be ({B}, V, V, V, 3), got {tuple(coords.shape)}")
+        V = coords.shape[1]
+        _require_gpu(feat, proj, coords, packed, scale, shift)
+    lib = _lib.load()
+    ws = torch.empty(lib.mvn_unproject_v2v_front_workspace_bytes(int(group_frames), V), dtype=torch.uint8,
+                     device=feat.device)
+    out = torch.empty((B, COUT, V, V, V), dtype=out_dtype, device=feat.device)
+    code = lib.mvn_unproject_v2v_front(feat.data_ptr(), fd, proj.data_ptr(),
+                                       coords.data_ptr() if coords is not None else None,
+                                       cub.params.data_ptr() if cub is not None else None,
+                                       int(cub.transfer) if cub is not None else 0, agg, int(align_corners),
+                                       packed.data_ptr(), scale.data_ptr(), shift.data_ptr(), out.data_ptr(), od,
+                                       ws.data_ptr(), ws.numel(), int(group_frames), B, N, C, H, W, V, _stream(feat))
+    _lib.check(code, "mvn_unproject_v2v_front")
+    return out

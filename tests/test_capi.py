@@ -111,3 +111,24 @@ def test_python_api_error_types_match_reference():
     with pytest.raises(AssertionError):                                                # multiview.py:143
         multiview.triangulate_batch_of_points(torch.zeros(1, 3, 3, 4), torch.zeros(1, 2, 5, 2))
     assert op.aggregation_code("conf_norm") == op.aggregation_code("conf")             # op.py:147
+
+
+def test_unproject_v2v_front_argument_validation(lib):
+    """The one-call config-5 pipeline: exactly one coordinate source, 32 channels, V % 16,
+    no 'conf' aggregation, a workspace of one group (no HIP call on these paths)."""
+    assert lib.mvn_unproject_v2v_front_workspace_bytes(8, 64) == 8 * 64 ** 3 * 32 * 2
+    assert lib.mvn_unproject_v2v_front_workspace_bytes(0, 64) == 8 * 64 ** 3 * 32 * 2     # default: 8 frames
+    ws = lib.mvn_unproject_v2v_front_workspace_bytes(2, 64)
+
+    def call(**k):
+        return lib.mvn_unproject_v2v_front(k.get("feat", 1), 0, 1, k.get("coords", 1), k.get("cub", None), 0,
+                                           k.get("agg", 2), 0, 1, 1, 1, 1, 0, k.get("ws", 1), k.get("wsb", ws),
+                                           2, 3, 4, k.get("C", 32), 96, 96, k.get("V", 64), None)
+    assert call(feat=None) == -1
+    assert call(coords=None) == -1                      # neither coordinate source
+    assert call(cub=1) == -1                            # both
+    assert call(agg=3) == -1                            # conf*
+    assert call(C=16) == -2
+    assert call(V=40) == -2
+    assert call(ws=None) == -5
+    assert call(wsb=ws - 1) == -5

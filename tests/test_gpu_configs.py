@@ -137,6 +137,31 @@ def test_cfg5_pipeline_full_size(device):
     assert_within_one_bf16_ulp(y16, y.cpu().numpy().astype(np.float64), 1e-30)
 
 
+@pytest.mark.parametrize("coords_kind", ("volume", "cuboids"))
+def test_cfg5_one_call_pipeline_equals_two_steps(device, coords_kind):
+    """mvn_unproject_v2v_front (frame groups through a one-group workspace) at V = 64 with a
+    ragged last group (3 frames in groups of 2) and the default grouping: bit-identical to
+    unproject_channels_last + v2v_front on the whole batch, f32 and bf16 outputs."""
+    from mvn_rocm import synth, v2v, volumetric
+    vb = synth.volumetric_batch(3, dtype=torch.bfloat16, device=device, seed=56)
+    coords = vb.coords
+    if coords_kind == "cuboids":
+        rng = np.random.default_rng(56)
+        base = rng.uniform(-500, 500, (3, 3)) + np.array([0, 0, 900.0])
+        coords = volumetric.build_cuboids(base, 2500.0, 64, rng.uniform(0, 2 * np.pi, 3), "coco", False, device=device)
+    g = torch.Generator().manual_seed(56)
+    w = torch.randn((16, 32, 7, 7, 7), generator=g) * 0.02
+    packed, scale, shift = v2v.fold_basic3d_block(w, torch.randn(16, generator=g) * 0.1, torch.rand(16, generator=g) + 0.5,
+                                                  torch.randn(16, generator=g) * 0.1, torch.zeros(16), torch.ones(16),
+                                                  device=device)
+    cl = v2v.unproject_channels_last(vb.features, vb.proj, coords, "softmax")
+    for od in (torch.float32, torch.bfloat16):
+        ref = v2v.v2v_front(cl, packed, scale, shift, od)
+        for gf in (2, 0):
+            got = v2v.unproject_v2v_front(vb.features, vb.proj, coords, packed, scale, shift, "softmax", od, gf)
+            assert torch.equal(got, ref), (od, gf)
+
+
 def test_v2v_front_two_frames_64(device):
     """Two frames at V = 64 (the x-column walk over 16 tiles, both frames' halos)."""
     import torch.nn.functional as F

@@ -28,7 +28,7 @@ for B, dt, label in ((8, torch.float32, "cfg2 f32"), (32, torch.bfloat16, "cfg3 
             assert lib.mvn_unproject(vb.features.data_ptr(), code, vb.proj.data_ptr(), vb.coords.data_ptr(), None,
                                      out.data_ptr(), code, B, 4, 32, 96, 96, 64, 64, 64, agg, 0, stream) == 0
         torch.cuda.synchronize()
-        nb = B * 512
+        nb = B * (64 ** 3 // (512 if code == 0 else 256))       # tile 4x8x16 (f32) / 4x8x8 (bf16)
         st = np.zeros(nb * 16, np.uint64)
         assert lib.mvn_x4_stamps(st.ctypes.data, st.nbytes) == 0
         st = st.reshape(nb, 16).astype(np.int64)
@@ -40,4 +40,9 @@ for B, dt, label in ((8, torch.float32, "cfg2 f32"), (32, torch.bfloat16, "cfg3 
         for k, n in enumerate(("consume", "commit (vmcnt + ds_write)", "barrier", "issue")):
             print(f"    loop:{n:26s} median {np.median(st[:, 8 + k]):8.0f}")
         rt = (st[:, 0] - st[:, 0].min()) / 100.0      # s_memrealtime: 100 MHz -> us
+        end = rt + tot / 2100.0                        # lifetime at ~2.1 GHz
+        span = end.max()
         print(f"    block starts span {rt.max():.1f} us; per-block lifetime at ~2.1 GHz = {np.median(tot) / 2100:.2f} us")
+        print(f"    estimated kernel span {span:.1f} us; last block start at {rt.max() / span:.3f} of it; "
+              f"blocks ending after 90 % of the span: {(end > 0.9 * span).sum()}; "
+              f"time with < half the block slots busy ~ {(span - np.percentile(end, 75)):.1f} us")

@@ -70,9 +70,6 @@ __device__ unsigned long long g_x4_stamps[1 << 21];
 #ifndef MVN_X4_TILE
 #define MVN_X4_TILE -1   // voxel tile: 0 = 4x8x16 (512 threads), 1 = 8x8x8 (512), 2 = 4x8x8 (256), -1 = per dtype
 #endif
-#ifndef MVN_X4_CORNER
-#define MVN_X4_CORNER 0  // 1: footprint boxes from the tile's corners (no barrier), else exact per voxel
-#endif
 #ifndef MVN_X4_XCD_MIN_FRAMES
 #define MVN_X4_XCD_MIN_FRAMES 1    // from this many frames each XCD takes the same slab of every frame
 #endif
@@ -87,9 +84,6 @@ __device__ unsigned long long g_x4_stamps[1 << 21];
 #endif
 #ifndef MVN_X4_CL_GROUPS
 #define MVN_X4_CL_GROUPS 4          // bf16 channels-last: channel groups per run of 16-byte stores (1, 2, 4)
-#endif
-#ifndef MVN_X4_ROWINT
-#define MVN_X4_ROWINT 0  // 1: chunks numbered over groups of 4 rows (conflict-free ds_write_b128)
 #endif
 
 namespace mvn {
@@ -127,7 +121,7 @@ __device__ __forceinline__ Region make_region(int x0, int y0, int bw, int bh, in
   r.cw = bw ? (x0 + bw - r.xa + 3) >> 2 : 0;                 // chunks per row
   // chunks are numbered over groups of 4 rows, rows fastest (see chunk_fields): rows padded
   // to a multiple of 4
-  r.cend = cbase + r.cw * (MVN_X4_ROWINT ? (bh + 3) & ~3 : bh);
+  r.cend = cbase + r.cw * bh;
   r.inv_cw = r.cw ? __builtin_amdgcn_rcpf(float(r.cw)) : 0.f;
   return r;
 }
@@ -207,44 +201,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
 
   if (t < 4) stage[(t >> 1) * kBuf + kZeroSlot + (t & 1)] = uint4{0u, 0u, 0u, 0u};
 
-  // ---- tile corners -> per-view footprint boxes (every wave for itself: no barrier) ----
-  // The voxel grid is an affine image of the integer lattice (a rotated cuboid,
-  // triangulation.py:280-341), and every voxel of the tile is in front of a camera whose
-  // 8 tile corners are: then the convex hull of the corners' projections contains every
-  // voxel's projection, so the bounding box of the corners (1e-3 px of slack for f32
-  // rounding) bounds the block's bilinear footprints.  Lanes 8v..8v+7 of lanes 0..31
-  // project corner (lane & 7) in view v.  Coordinate volumes that are not affine grids are
-  // caught per voxel below (a voxel outside its box is recomputed by global gathers); a
-  // tile that reaches behind a camera uses the exact per-voxel box (one barrier).
   const int X0 = tx * TX, Y0 = ty * TY, Z0 = tz * TZ;
-  float cbox[4] = {0.f, 0.f, 0.f, 0.f};   // min x, max x, min y, max y (reduced over 8 lanes)
-  bool corner_ok = false;
-  if (MVN_X4_CORNER) {
-    const int c = lane & 7, v = (lane >> 3) & 3;
-    const int Xc = X0 + ((c & 4) ? min(TX, Vx - X0) - 1 : 0);
-    const int Yc = Y0 + ((c & 2) ? min(TY, Vy - Y0) - 1 : 0);
-    const int Zc = Z0 + ((c & 1) ? min(TZ, Vz - Z0) - 1 : 0);
-    float o[3];
-    if (cub) {
-      cuboid_coord(cub + b * MVN_CUBOID_FLOATS, Vx, Xc, Yc, Zc, transfer, o);
-    } else {
-      const float* cp = coords + (size_t(b) * nvox + (size_t(Xc) * Vy + Yc) * Vz + Zc) * 3;
-      o[0] = cp[0]; o[1] = cp[1]; o[2] = cp[2];
-    }
-    const Homog hp = homog(Pb + v * 12, o[0], o[1], o[2]);
-    const Recip rH0 = recip_refined(float(H)), rW0 = recip_refined(float(W));
-    const Proj pc = project_h<false>(hp, H, W, align_corners, rH0, rW0);
-    bool ok = (hp.wh > 0.f) && (fabsf(pc.ix) < 0x1p24f) && (fabsf(pc.iy) < 0x1p24f);
-    cbox[0] = pc.ix - 1e-3f; cbox[1] = pc.ix + 1e-3f; cbox[2] = pc.iy - 1e-3f; cbox[3] = pc.iy + 1e-3f;
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) {
-      cbox[0] = fminf(cbox[0], __shfl_xor(cbox[0], m, kWave));
-      cbox[1] = fmaxf(cbox[1], __shfl_xor(cbox[1], m, kWave));
-      cbox[2] = fminf(cbox[2], __shfl_xor(cbox[2], m, kWave));
-      cbox[3] = fmaxf(cbox[3], __shfl_xor(cbox[3], m, kWave));
-    }
-    corner_ok = (__builtin_amdgcn_ballot_w64(!ok) & 0xffffffffull) == 0;
-  }
 
   // ---- this thread's voxel ------------------------------------------------------------
   // A wave takes 64 / TZ consecutive y-rows of one x-plane.  A ds_read_b128 is serviced in
@@ -307,15 +264,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   // ---- per-view boxes (ints, clipped to the pixels a tap can start at) ----------------
   int box[NV][4];
   X4_STAMP(2);
-  if (MVN_X4_CORNER && corner_ok) {
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      box[v][0] = max(int(floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cbox[0]), 8 * v)))), -1);
-      box[v][1] = min(int(floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cbox[1]), 8 * v)))), W - 1);
-      box[v][2] = max(int(floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cbox[2]), 8 * v)))), -1);
-      box[v][3] = min(int(floorf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cbox[3]), 8 * v)))), H - 1);
-    }
-  } else {
+  {
     // exact: every voxel's base pixel.  The 16 per-wave reductions (4 views x min x0, max x1,
     // min y0, max y1; maxima as minima of negated values) run as one transposing butterfly:
     // lanes 32 apart swap halves of their 16 values (v_permlane32_swap), then rows 16 apart
@@ -414,20 +363,15 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   const bool lds_out = kLdsOut && !out_cl && (X0 + TX <= Vx) && (Y0 + TY <= Vy) && (Z0 + TZ <= Vz);
   const uint32_t ooff_cl = act ? uint32_t(vox) * uint32_t(C) * uint32_t(sizeof(TOut)) : kOob;
 
-  // LDS byte offsets of each view's north-west and south-west taps; a voxel whose base
-  // pixel falls outside its view's box (only possible for a coordinate volume that is not
-  // an affine grid) samples the zero slots and is recomputed by global gathers at the end.
+  // LDS byte offsets of each view's north-west and south-west taps (the exact boxes contain
+  // every voxel's base pixel by construction; voxels that sample nothing read the zero slots)
   uint32_t anw[NV], asw[NV];
-  bool refix = false;
   auto tap_slots = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const Region rv = rs.get(v);
       const int dx = fx[v] - rv.x0, dy = fy[v] - rv.y0;
-      // (exact boxes contain every voxel's base pixel by construction)
-      const bool inbox = !MVN_X4_CORNER || ((dx >= 0) & (dx <= rv.bw - 2) & (dy >= 0) & (dy <= rv.bh - 2));
-      if (MVN_X4_CORNER) refix |= has[v] & !inbox;             // (has implies act)
-      const bool use = has[v] & inbox;
+      const bool use = has[v];
       const int slot = rv.sbase + dy * rv.pitch + dx;
       anw[v] = uint32_t(use ? slot : kZeroSlot) * kSlotB;
       asw[v] = uint32_t(use ? slot + rv.pitch : kZeroSlot) * kSlotB;
@@ -437,43 +381,13 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       }
     }
   };
-  // (coordinates re-derived here, so that nothing of the prologue stays live through the
-  // channel loop for this rare path)
-  auto fix_voxel = [&]() __attribute__((always_inline)) {
-    if (MVN_X4_CORNER && refix) {
-      const int Xr = X0 + vt / (TZ * TY), Yr = Y0 + (vt / TZ) % TY;
-      const int Zr = Z0 + vt % TZ;
-      const int vr = (Xr * Vy + Yr) * Vz + Zr;
-      float o[3];
-      if (cub) {
-        cuboid_coord(cub + b * MVN_CUBOID_FLOATS, Vx, Xr, Yr, Zr, transfer, o);
-      } else {
-        const float* cp = coords + (size_t(b) * nvox + vr) * 3;
-        o[0] = cp[0]; o[1] = cp[1]; o[2] = cp[2];
-      }
-      gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + (out_cl ? size_t(vr) * C : vr),
-                                   out_cl ? 1 : nvox, NV, C, H, W, o[0], o[1], o[2], align_corners);
-    }
-  };
-
   // Chunk (k of a pass) -> global byte offset (kOob outside the image), first LDS slot and
   // the mask of its 4 pixels that lie in the view's box (empty past the pass's chunks).
   auto chunk_fields = [&](const Region& r, int sel, int li, uint32_t& goff, int& s0, uint32_t& mask, bool live)
       __attribute__((always_inline)) {
-    // li = (row group * cw + chunk column) * 4 + row in group: the 8 lanes of a
-    // ds_write_b128 lane group then cover 4 rows x 2 chunks, whose slots differ by an odd
-    // pitch between rows and by 4 between chunks — 8 distinct 16-byte bank groups, where
-    // 8 chunks of one row would hit only two (4-way conflicts).
-#if MVN_X4_ROWINT
-    const int q = li >> 2;
-    const int grp = int((float(q) + 0.5f) * r.inv_cw);
-    const int py = 4 * grp + (li & 3);
-    live &= py < r.bh;
-    const int gx = r.xa + 4 * (q - grp * r.cw), gy = r.y0 + py;
-#else
+    // li = row * cw + chunk column (rows fastest-varying outer)
     const int py = int((float(li) + 0.5f) * r.inv_cw);
     const int gx = r.xa + 4 * (li - py * r.cw), gy = r.y0 + py;
-#endif
     const bool in = live & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H);
     goff = in ? uint32_t((sel * C * HW + gy * W + gx) * int(E)) : kOob;
     s0 = r.sbase + py * r.pitch + (gx - r.x0);
@@ -679,7 +593,6 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     }
     X4_STAMP(7);
     X4_ACC_STORE;
-    fix_voxel();
     return;
   }
 
@@ -708,7 +621,6 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     }
     aggregate_store(c0, sv, false);
   }
-  fix_voxel();
 }
 
 }  // namespace

@@ -203,11 +203,45 @@ def dtype_name(dt):
     return {torch.float32: "f32", torch.bfloat16: "bf16"}[dt]
 
 
-def roofline(c, r, cfg_name):
+_COPY_GBPS = None
+
+
+def copy_bandwidth(device):
+    """Measured device-to-device copy bandwidth (SURVEY.md §8d asks for the fraction of it
+    next to the spec peak): a 1 GiB f32 buffer copied back to back, bytes read + written
+    per second, best of 3 x 20 copies after ~0.3 s of settling."""
+    global _COPY_GBPS
+    if _COPY_GBPS is None:
+        import torch
+        n = (1 << 30) // 4
+        src = torch.empty(n, device=device).normal_()
+        dst = torch.empty_like(src)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.3:
+            dst.copy_(src)
+        best = float("inf")
+        for _ in range(3):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(20):
+                dst.copy_(src)
+            e.record()
+            torch.cuda.synchronize()
+            best = min(best, s.elapsed_time(e) / 20)
+        _COPY_GBPS = 2 * n * 4 / (best * 1e-3) / 1e9
+        del src, dst
+    return _COPY_GBPS
+
+
+def roofline(c, r, cfg_name, device=None):
     traffic, src = measured_traffic(cfg_name)
-    return {"kernel": kernel_name(c), "bound": "hbm", "achieved": r["achieved_gbps"], "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s", "frac": r["achieved_gbps"] / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": src,
-            "launch_ms": r["unproject_ms"], "algorithmic_bytes_per_launch": r["launch_bytes"]}
+    out = {"kernel": kernel_name(c), "bound": "hbm", "achieved": r["achieved_gbps"], "peak": HBM_PEAK_GBPS,
+           "unit": "GB/s", "frac": r["achieved_gbps"] / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": src,
+           "launch_ms": r["unproject_ms"], "algorithmic_bytes_per_launch": r["launch_bytes"]}
+    if device is not None:
+        cp = copy_bandwidth(device)
+        out.update(measured_copy_gbps=cp, frac_of_measured_copy=r["achieved_gbps"] / cp)
+    return out
 
 
 # ----------------------------------------------------------------------------- workloads
@@ -503,7 +537,7 @@ def main():
         s = run_config("3", args, rank, world, device, clock)
         secondary = dict(workload=s["cfg"]["label"], value=s["fps"], unit="frames/s", ms_per_step=s["ms_per_step"],
                          frames_per_gpu=s["cfg"]["frames"], dtype="bf16", unproject_ms=s["unproject_ms"],
-                         softargmax_ms=s["softargmax_ms"], roofline=roofline(s["cfg"], s, "3"),
+                         softargmax_ms=s["softargmax_ms"], roofline=roofline(s["cfg"], s, "3", device),
                          path_algorithmic_gbps=s["path_gbps"], path_frac=s["path_gbps"] / HBM_PEAK_GBPS)
     if not args.no_secondary and not args.no_in_kernel_coords:
         # the same workload with the coordinate volume formed inside both kernels from the
@@ -557,9 +591,10 @@ def main():
                        "views": c["views"], "channels": c["channels"], "heatmap": c["heatmap"],
                        "volume": c["volume"], "joints": c["joints"], "parallelism": f"dp{world}",
                        "collective": "all_gather joints (RCCL)" if world > 1 else None},
-            "roofline": roofline(c, r, args.config),
+            "roofline": roofline(c, r, args.config, device),
             "softargmax_ms": r["softargmax_ms"],
             "path_algorithmic_gbps": r["path_gbps"],
+            "path_frac": r["path_gbps"] / HBM_PEAK_GBPS,
             "cpu_baseline": base,
             "secondary": secondary,
             "config1": config1,

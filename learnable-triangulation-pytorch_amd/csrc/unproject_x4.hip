@@ -143,10 +143,17 @@ template <> struct RegionSet<true> {
                        int((c >> 13) & 0x7ffu), int(c >> 24));
   }
   __device__ __forceinline__ Region get(int v) const { return unpack(a[v], b[v], c[v]); }
+  // u per lane: plain selects (9 v_cndmask).  Not through readfirstlane as pick_region does:
+  // a convergent op cannot be speculated, so each select became a branch tree with exec
+  // masking (~4,200 cycles of block prologue at config 2, profiles/r13_x4_stamps.txt).
   __device__ __forceinline__ Region pick(int u) const {
-    const uint32_t pa = u == 0 ? rfl(int(a[0])) : u == 1 ? rfl(int(a[1])) : u == 2 ? rfl(int(a[2])) : rfl(int(a[3]));
-    const uint32_t pb = u == 0 ? rfl(int(b[0])) : u == 1 ? rfl(int(b[1])) : u == 2 ? rfl(int(b[2])) : rfl(int(b[3]));
-    const uint32_t pc = u == 0 ? rfl(int(c[0])) : u == 1 ? rfl(int(c[1])) : u == 2 ? rfl(int(c[2])) : rfl(int(c[3]));
+    uint32_t pa = a[0], pb = b[0], pc = c[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      pa = u == k ? a[k] : pa;
+      pb = u == k ? b[k] : pb;
+      pc = u == k ? c[k] : pc;
+    }
     return unpack(pa, pb, pc);
   }
 };
@@ -541,6 +548,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       const Region r = rs.pick(sel);
       chunk_fields(r, sel, k - r.cbase, goff[i], s0[i], mask[i], k < total);
     }
+    X4_STAMP(12);
     const int wfirst = __builtin_amdgcn_readfirstlane(wid * kWave);
     Chunk pre[MC][G];
     auto issue = [&](int c0) __attribute__((always_inline)) {

@@ -37,6 +37,7 @@ for B, dt, label in ((8, torch.float32, "cfg2 f32"), (32, torch.bfloat16, "cfg3 
         print(f"{label} agg={agg}: blocks {nb}, block lifetime median {np.median(tot):.0f} cyc, mean {tot.mean():.0f}")
         for i, n in enumerate(names):
             print(f"    {n:14s} median {np.median(d[:, i]):8.0f}  mean {d[:, i].mean():8.0f}  p90 {np.percentile(d[:, i], 90):8.0f}")
+        print(f"    (chunk descriptors alone: median {np.median(st[:, 12] - st[:, 4]):8.0f}; first issue {np.median(st[:, 5] - st[:, 12]):8.0f})")
         for k, n in enumerate(("consume", "commit (vmcnt + ds_write)", "barrier", "issue")):
             print(f"    loop:{n:26s} median {np.median(st[:, 8 + k]):8.0f}")
         rt = (st[:, 0] - st[:, 0].min()) / 100.0      # s_memrealtime: 100 MHz -> us

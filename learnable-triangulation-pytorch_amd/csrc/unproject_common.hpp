@@ -298,8 +298,18 @@ __device__ __forceinline__ uint32_t chunk_px(const uint2& q, int p) {
   return (p & 1) ? (d & 0xffff0000u) : (d << 16);      // bf16 -> f32 bits, exact
 }
 
+// bf16 maps staged as bf16 (unproject_x4.hip, 8-byte slots): pixel p (0..3) of chunks ca, cb
+// as one word, channel a low (v_perm_b32 of the two halves)
+__device__ __forceinline__ uint32_t chunk_pair(const uint2& ca, const uint2& cb, int p) {
+  return __builtin_amdgcn_perm(p < 2 ? cb.x : cb.y, p < 2 ? ca.x : ca.y, (p & 1) ? 0x07060302u : 0x05040100u);
+}
+
 __device__ __forceinline__ f2 lo2(const uint4& q) { return f2{__uint_as_float(q.x), __uint_as_float(q.y)}; }
 __device__ __forceinline__ f2 hi2(const uint4& q) { return f2{__uint_as_float(q.z), __uint_as_float(q.w)}; }
+// channels (0, 1) / (2, 3) of an 8-byte slot of 4 bf16 channels, widened to f32 (exact)
+__device__ __forceinline__ f2 bf16_pair(uint32_t d) { return f2{__uint_as_float(d << 16), __uint_as_float(d & 0xffff0000u)}; }
+__device__ __forceinline__ f2 lo2(const uint2& q) { return bf16_pair(q.x); }
+__device__ __forceinline__ f2 hi2(const uint2& q) { return bf16_pair(q.y); }
 
 // View aggregation of a channel pair (op.py:147-161), lane-wise the op order of
 // aggregate<> (sum / max / conf, reference order; softmax, the unified formula).

@@ -24,6 +24,8 @@
 // in flight, XCD-balanced block order, buffer-descriptor stores — follows unproject_tiled.
 // Footprints that exceed one LDS buffer are staged in several passes of whole views;
 // a single view larger than a buffer sends its block to the global-gather fallback.
+#include <type_traits>
+
 #include "unproject_common.hpp"
 
 // Ablation switches for A/B builds (tools/build_x4_variant.sh); all 0 in the library.
@@ -82,6 +84,9 @@ __device__ unsigned long long g_x4_stamps[1 << 21];
 #ifndef MVN_X4_PATCH_LANES
 #define MVN_X4_PATCH_LANES 1        // lane groups of ds_read_b128 take compact 2 x 8 (y, z) voxel patches
 #endif
+#ifndef MVN_X4_BF16_LDS
+#define MVN_X4_BF16_LDS 0           // 1: bf16 maps staged as bf16, 8-byte LDS slots of 4 channels
+#endif                              //    (bit-identical; cfg3 533 -> 570 us: the widening VALU costs more)
 #ifndef MVN_X4_CL_GROUPS
 #define MVN_X4_CL_GROUPS 4          // bf16 channels-last: channel groups per run of 16-byte stores (1, 2, 4)
 #endif
@@ -171,10 +176,15 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   // per buffer: image slots [0, kTrash), 64 per-lane trash slots (the masked-off pixels of
   // a chunk are written there: no exec-mask branch per write), 2 zero slots
   constexpr int kZeroSlot = kBuf - 2, kTrash = kBuf - 2 - kWave;
-  constexpr uint32_t kSlotB = 16;
+  // LDS slot = one pixel's G channels: f32 (16 bytes), or bf16 maps kept as bf16 (8 bytes:
+  // half the LDS bytes written and read per channel; a tap's pairs are widened to f32 on the
+  // read side, exactly)
+  constexpr bool kB16 = MVN_X4_BF16_LDS && sizeof(TIn) == 2;
+  using Slot = typename std::conditional<kB16, uint2, uint4>::type;
+  constexpr uint32_t kSlotB = sizeof(Slot);
   constexpr uint32_t E = sizeof(TIn);
 
-  __shared__ uint4 stage[2 * kBuf];
+  __shared__ Slot stage[2 * kBuf];
   __shared__ int red[kWaves][NV][4];
   // bf16 NCDHW output: each group's G channel planes of the tile gathered in LDS (double
   // buffered), then stored as 16-byte rows (TZ = 8 voxels) one barrier later — instead of
@@ -206,7 +216,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   const TIn* fb = feat + size_t(b) * NV * C * HW;
   const float* cfb = conf ? conf + size_t(b) * NV * C : nullptr;
 
-  if (t < 4) stage[(t >> 1) * kBuf + kZeroSlot + (t & 1)] = uint4{0u, 0u, 0u, 0u};
+  if (t < 4) stage[(t >> 1) * kBuf + kZeroSlot + (t & 1)] = Slot{};
 
   const int X0 = tx * TX, Y0 = ty * TY, Z0 = tz * TZ;
 
@@ -412,10 +422,14 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   };
   // masked-off pixels: bf16 maps write them to the lane's trash slot (no exec-mask branch
   // per write), f32 maps branch (A/B at the bench configs: each is the faster for its dtype)
-  auto write_group = [&](uint4* buf, const Chunk (&pre)[G], int s0, uint32_t mask) __attribute__((always_inline)) {
+  auto write_group = [&](Slot* buf, const Chunk (&pre)[G], int s0, uint32_t mask) __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const uint4 q = make_uint4(chunk_px(pre[0], p), chunk_px(pre[1], p), chunk_px(pre[2], p), chunk_px(pre[3], p));
+      Slot q;
+      if constexpr (kB16)
+        q = make_uint2(chunk_pair(pre[0], pre[1], p), chunk_pair(pre[2], pre[3], p));
+      else
+        q = make_uint4(chunk_px(pre[0], p), chunk_px(pre[1], p), chunk_px(pre[2], p), chunk_px(pre[3], p));
       if constexpr (sizeof(TIn) == 2)
         buf[(mask & (1u << p)) ? s0 + p : kTrash + lane] = q;
       else if (mask & (1u << p))
@@ -428,10 +442,10 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (!all && rs.get(v).pass != pass) continue;
-      const uint4 a = *reinterpret_cast<const uint4*>(buf + anw[v]);
-      const uint4 bq = *reinterpret_cast<const uint4*>(buf + anw[v] + kSlotB);
-      const uint4 cq = *reinterpret_cast<const uint4*>(buf + asw[v]);
-      const uint4 d = *reinterpret_cast<const uint4*>(buf + asw[v] + kSlotB);
+      const Slot a = *reinterpret_cast<const Slot*>(buf + anw[v]);
+      const Slot bq = *reinterpret_cast<const Slot*>(buf + anw[v] + kSlotB);
+      const Slot cq = *reinterpret_cast<const Slot*>(buf + asw[v]);
+      const Slot d = *reinterpret_cast<const Slot*>(buf + asw[v] + kSlotB);
       const f2 w0{w[v][0], w[v][0]}, w1{w[v][1], w[v][1]}, w2{w[v][2], w[v][2]}, w3{w[v][3], w[v][3]};
       sv[0][v] = pk_fma(lo2(d), w3, pk_fma(lo2(cq), w2, pk_fma(lo2(bq), w1, lo2(a) * w0)));
       sv[1][v] = pk_fma(hi2(d), w3, pk_fma(hi2(cq), w2, pk_fma(hi2(bq), w1, hi2(a) * w0)));
@@ -526,7 +540,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     }
   };
 
-  auto consume = [&](const uint4* buf, int c0) __attribute__((always_inline)) {
+  auto consume = [&](const Slot* buf, int c0) __attribute__((always_inline)) {
     f2 sv[2][NV];
     sample_views(reinterpret_cast<const char*>(buf), true, 0, sv);
     aggregate_store(c0, sv, lds_out);         // (single-pass loop: rows flushed after the barrier)
@@ -558,7 +572,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
         if (wfirst + kThreads * i < total) load_group(pre[i], goff[i], c0);
     };
     int ncommit = 0;
-    auto commit = [&](uint4* buf) __attribute__((always_inline)) {
+    auto commit = [&](Slot* buf) __attribute__((always_inline)) {
       if (MVN_X4_ABL_NOSTAGE && ncommit++ >= 2) return;
 #pragma unroll
       for (int i = 0; i < MC; ++i)

@@ -200,8 +200,8 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     for (int r = 0; r < RUNS; ++r)
       load_run<T, VEC>(vb + j * jstride, chunk * kPartChunk + r * kWave * VEC + lane * VEC, nvox, vec_ok, x[r], fill);
   };
-  // One joint's 5-float partial from its (multiplier-scaled) values.
-  auto reduce_joint = [&](int j, float (&x)[RUNS][VEC]) __attribute__((always_inline)) {
+  // One joint's 5-float partial from its (multiplier-scaled) values, wave-uniform in q.
+  auto reduce_values = [&](float (&x)[RUNS][VEC], float (&q)[kPartial]) __attribute__((always_inline)) {
     float m = 0.f, s = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
     if constexpr (SOFTMAX) {
       constexpr float kLog2e = 1.4426950408889634f;
@@ -237,13 +237,89 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
         }
     }
     s = wave_sum63(s); sx = wave_sum63(sx); sy = wave_sum63(sy); sz = wave_sum63(sz);
+    auto l63 = [](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), kWave - 1)); };
+    q[0] = m; q[1] = l63(s); q[2] = l63(sx); q[3] = l63(sy); q[4] = l63(sz);
+  };
+  auto reduce_joint = [&](int j, float (&x)[RUNS][VEC]) __attribute__((always_inline)) {
+    float q[kPartial];
+    reduce_values(x, q);
     if (lane == kWave - 1) {
       float* o = part + ((size_t(b) * J + j) * nchunk + chunk) * kPartial;
-      o[0] = m; o[1] = s; o[2] = sx; o[3] = sy; o[4] = sz;
+#pragma unroll
+      for (int k = 0; k < kPartial; ++k) o[k] = q[k];
     }
   };
 
   const int i0 = chunk * kPartChunk + lane * VEC;
+  const size_t frame_bytes = (size_t(J - 1) * size_t(jstride) + size_t(nvox)) * sizeof(T);
+  if (vec_ok && chunk * kPartChunk + kPartChunk <= nvox && J <= kWave && frame_bytes < (size_t(1) << 31) &&
+      jstride * sizeof(T) < (1u << 31)) {
+    // Full chunk, aligned, frame addressable by a buffer descriptor: the raw 16-byte loads
+    // of PF joints in flight (a ring of register sets refilled PF joints ahead), issued
+    // UNCONDITIONALLY (past the last joint the offset is out of range: no memory access),
+    // and no stores inside the joint loop — each joint's partial is parked in lane j % 64 of
+    // five registers and the lanes store together after the loop.  gfx950's vmcnt counts
+    // loads and stores in issue order: a conditional load or a divergent store in the loop
+    // made the compiler's waits conservative (vmcnt(0) at every ring turn, draining the
+    // prefetch ring).  J <= 64 (one lane per joint); more joints take the path below.
+    constexpr int PF = sizeof(T) == 2 ? 8 : 4;
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T*>(vb), 0, int(frame_bytes), 0x00020000);
+    uint4 raw[PF][RUNS];
+    auto issue = [&](int j, uint4 (&q)[RUNS]) __attribute__((always_inline)) {
+      const uint32_t jo = j < J ? uint32_t(j) * uint32_t(jstride) * uint32_t(sizeof(T)) : 0x80000000u;
+#pragma unroll
+      for (int r = 0; r < RUNS; ++r)
+        q[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             vrs, uint32_t((i0 + r * kWave * VEC) * sizeof(T)), jo, 0));
+    };
+    float acc[kPartial] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    auto flush = [&](int jbase, int n) __attribute__((always_inline)) {
+      if (lane < n) {
+        float* o = part + ((size_t(b) * J + jbase + lane) * nchunk + chunk) * kPartial;
+#pragma unroll
+        for (int k = 0; k < kPartial; ++k) o[k] = acc[k];
+      }
+    };
+    // ring slots filled in joint order (the scheduler otherwise reverses them, and the wait
+    // analysis then merges "slot 0 issued last" into the loop: vmcnt at every ring turn)
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      issue(p, raw[p]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    for (int j0 = 0; j0 < J; j0 += PF) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        const int j = j0 + p;
+        if (j >= J) goto joints_done;     // an exit edge, not a merge into the loop latch
+        float x[RUNS][VEC];
+#pragma unroll
+        for (int r = 0; r < RUNS; ++r) {
+          const uint32_t w[4] = {raw[p][r].x, raw[p][r].y, raw[p][r].z, raw[p][r].w};
+          if constexpr (sizeof(T) == 4) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[r][k] = __uint_as_float(w[k]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              x[r][2 * k] = __uint_as_float(w[k] << 16);
+              x[r][2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+            }
+          }
+        }
+        issue(j + PF, raw[p]);
+        float q[kPartial];
+        reduce_values(x, q);
+        const bool mine = lane == (j & (kWave - 1));
+#pragma unroll
+        for (int k = 0; k < kPartial; ++k) acc[k] = mine ? q[k] : acc[k];
+      }
+    }
+  joints_done:
+    flush(0, J);
+    return;
+  }
   if (vec_ok && chunk * kPartChunk + kPartChunk <= nvox) {
     // Full chunk, aligned: the raw 16-byte loads of PF joints in flight (a ring of register
     // sets refilled PF joints ahead), widened only when their joint is reduced.  One joint

@@ -194,6 +194,21 @@ __device__ __forceinline__ float aggregate(const float (&s)[NV], int N, const fl
 
 constexpr uint32_t kOob = 0x80000000u;            // buffer byte offset past any frame
 
+// 16-byte buffer store followed by two wait states.  A VMEM store of more than 8 bytes reads
+// its data VGPRs after issue; a VALU write to them in the next cycles (cdna_asm_programming.md
+// §4.1 rows 8/9) makes the store write the NEW value.  hipcc left that pair unpadded in the
+// bf16 channels-last unprojection (a register copy right after the store: channels 14-15
+// nondeterministic, r14; tools/check_store_hazard.py scans the assembly for it), so every
+// 16-byte store goes through here.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <int AUX = 0>
+__device__ __forceinline__ void store_b128_padded(u32x4_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, AUX);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // Wave-wide integer min / max, returned wave-uniform.  row_shr DPP steps (identity
 // shifted in) leave each row's reduction in its lane 15; four readlanes combine the rows.
 __device__ __forceinline__ int wave_min_u(int v) {

@@ -362,11 +362,11 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
         else
           __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(r[0], r[1]), ors, ooff_cl, soff, 0);
       } else if constexpr (sizeof(TOut) == 4) {
-        __builtin_amdgcn_raw_buffer_store_b128(
+        store_b128_padded(
             __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
                                make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]),
                                           __float_as_uint(r[3]))),
-            ors, ooff_cl, soff, 0);
+            ors, ooff_cl, soff);
       } else {
         __builtin_amdgcn_raw_buffer_store_b64(
             __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int,

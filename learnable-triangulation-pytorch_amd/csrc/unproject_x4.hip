@@ -76,8 +76,10 @@ __device__ unsigned long long g_x4_stamps[1 << 21];
 #define MVN_X4_XCD_MIN_FRAMES 1    // from this many frames each XCD takes the same slab of every frame
 #endif
 #ifndef MVN_X4_LDS_STORE
-#define MVN_X4_LDS_STORE 1          // bf16 NCDHW output: rows of TZ voxels gathered in LDS, 16-byte stores
-#endif
+#define MVN_X4_LDS_STORE 0          // 1: bf16 NCDHW output rows of TZ voxels gathered in LDS, 16-byte
+#endif                              //    stores (r10: 583 -> 567 us at config 3; since the stores are
+                                    //    deferred past the next commit the direct 2-byte stores win:
+                                    //    542 -> 530 us, profiles/r14_ab.txt)
 #ifndef MVN_X4_LDS_STORE_POLICY
 #define MVN_X4_LDS_STORE_POLICY 0   // cache policy of those 16-byte stores (2 = nt)
 #endif
@@ -455,8 +457,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   uint2 cl_buf[MVN_X4_CL_GROUPS > 1 ? MVN_X4_CL_GROUPS - 1 : 1];
 #pragma unroll
   for (int k = 0; k < (MVN_X4_CL_GROUPS > 1 ? MVN_X4_CL_GROUPS - 1 : 1); ++k) cl_buf[k] = make_uint2(0u, 0u);
-  auto aggregate_store = [&](int c0, const f2 (&sv)[2][NV], bool to_lds) __attribute__((always_inline)) {
-    float r[G];
+  auto aggregate = [&](int c0, const f2 (&sv)[2][NV], float (&r)[G]) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       f2 cf[NV];
@@ -468,8 +469,13 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       r[2 * q] = o.x;
       r[2 * q + 1] = o.y;
     }
+  };
+  // The group's G output values of this voxel: to global memory, or (bf16 NCDHW tiles) to
+  // the LDS row buffer that flush() stores after the next barrier.
+  auto store_out = [&](int c0, const float (&r)[G], bool to_lds) __attribute__((always_inline)) {
     if (out_cl) {
-      const uint32_t soff = uint32_t(c0) * uint32_t(sizeof(TOut));
+      // c0 is block-uniform; readfirstlane keeps it scalar (soffset operands must be SGPRs)
+      const uint32_t soff = __builtin_amdgcn_readfirstlane(uint32_t(c0) * uint32_t(sizeof(TOut)));
       if constexpr (sizeof(TOut) == 2 && MVN_X4_CL_GROUPS > 1) {
         // bf16 channels-last: MVN_X4_CL_GROUPS groups' 8-byte pieces of the voxel's record are
         // held in registers and go out as 16-byte stores of consecutive channels
@@ -480,10 +486,10 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
 #pragma unroll
           for (int k = 0; k + 1 < NG; k += 2) {
             const uint2 hi = k + 1 == NG - 1 ? cur : cl_buf[k + 1];
-            __builtin_amdgcn_raw_buffer_store_b128(
+            store_b128_padded(
                 __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
                                    make_uint4(cl_buf[k].x, cl_buf[k].y, hi.x, hi.y)),
-                ors, ooff_cl, soff - uint32_t((NG - 1 - k) * G * sizeof(TOut)), 0);
+                ors, ooff_cl, soff - uint32_t((NG - 1 - k) * G * sizeof(TOut)));
           }
         } else if (c0 + G >= C) {            // C / G not a multiple of NG: the tail group by itself
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, cur),
@@ -502,11 +508,11 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
         return;
       }
       if constexpr (sizeof(TOut) == 4)
-        __builtin_amdgcn_raw_buffer_store_b128(
+        store_b128_padded(
             __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
                                make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]),
                                           __float_as_uint(r[3]))),
-            ors, ooff_cl, soff, 0);
+            ors, ooff_cl, soff);
       else
         __builtin_amdgcn_raw_buffer_store_b64(
             __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int,
@@ -533,17 +539,20 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       const int ch = t / (TX * TY), row = t - ch * (TX * TY);
       const uint4 q = *reinterpret_cast<const uint4*>(ost + ((c0 / G) & 1) * (G * kThreads) + ch * kThreads + row * TZ);
       const int x = row / TY, y = row - x * TY;
-      const uint32_t voff = uint32_t(((X0 + x) * Vy + (Y0 + y)) * Vz + Z0) * uint32_t(sizeof(TOut));
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, q),
-                                             ors, voff, uint32_t(c0 + ch) * uint32_t(nvox) * uint32_t(sizeof(TOut)),
-                                             MVN_X4_LDS_STORE_POLICY);
+      // the lane's channel plane goes in the VGPR offset, the group's first plane in the
+      // scalar one (a per-lane soffset compiles into a readfirstlane waterfall loop)
+      const uint32_t voff = uint32_t(((X0 + x) * Vy + (Y0 + y)) * Vz + Z0) * uint32_t(sizeof(TOut)) +
+                            uint32_t(ch) * uint32_t(nvox) * uint32_t(sizeof(TOut));
+      const uint32_t soff = __builtin_amdgcn_readfirstlane(uint32_t(c0) * uint32_t(nvox) * uint32_t(sizeof(TOut)));
+      store_b128_padded<MVN_X4_LDS_STORE_POLICY>(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, q),
+                                                 ors, voff, soff);
     }
   };
 
-  auto consume = [&](const Slot* buf, int c0) __attribute__((always_inline)) {
+  auto consume = [&](const Slot* buf, int c0, float (&r)[G]) __attribute__((always_inline)) {
     f2 sv[2][NV];
     sample_views(reinterpret_cast<const char*>(buf), true, 0, sv);
-    aggregate_store(c0, sv, lds_out);         // (single-pass loop: rows flushed after the barrier)
+    aggregate(c0, sv, r);
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -585,25 +594,33 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     __syncthreads();
     X4_STAMP(6);
     X4_ACC_DECL;
+    // A group's outputs are stored after the NEXT group's commit: on gfx950 vmcnt counts
+    // stores as well as loads, in issue order, so stores issued at the end of a consume made
+    // the commit's wait for the next group's loads also wait for their write acknowledgement.
     int last = 0;
+    float r[G];
     for (int c0 = 0; c0 < C; c0 += 2 * G) {
       const bool more1 = c0 + G < C, more2 = c0 + 2 * G < C;
       if (more1) issue(c0 + G);
       X4_ACC(3);
-      consume(stage, c0);
+      consume(stage, c0, r);
       X4_ACC(0);
-      if (!more1) { last = c0; break; }
+      if (!more1) { store_out(c0, r, lds_out); last = c0; break; }
       commit(stage + kBuf);
+      __builtin_amdgcn_sched_barrier(0);
+      store_out(c0, r, lds_out);
       X4_ACC(1);
       __syncthreads();
       flush(c0);
       X4_ACC(2);
       if (more2) issue(c0 + 2 * G);
       X4_ACC(3);
-      consume(stage + kBuf, c0 + G);
+      consume(stage + kBuf, c0 + G, r);
       X4_ACC(0);
-      if (!more2) { last = c0 + G; break; }
+      if (!more2) { store_out(c0 + G, r, lds_out); last = c0 + G; break; }
       commit(stage);
+      __builtin_amdgcn_sched_barrier(0);
+      store_out(c0 + G, r, lds_out);
       X4_ACC(1);
       __syncthreads();
       flush(c0 + G);
@@ -641,7 +658,9 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       sample_views(reinterpret_cast<const char*>(stage), false, pass, sv);
       __syncthreads();
     }
-    aggregate_store(c0, sv, false);
+    float r[G];
+    aggregate(c0, sv, r);
+    store_out(c0, r, false);
   }
 }
 

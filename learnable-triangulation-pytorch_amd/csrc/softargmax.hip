@@ -13,6 +13,8 @@
 //           rescale), writes the coordinates and (max, 1/sum).
 //   pass 3  softargmax_finalize : one block per (4096-voxel chunk, joint, frame) streams
 //           the normalised volume (skipped when the caller does not want it).
+#include <algorithm>
+
 #include "common.hpp"
 
 // The finalize is the volume's last reader and its output is written once: both streams
@@ -43,6 +45,10 @@ constexpr int kPartial = 5;                     // m, s, sx, sy, sz
 #endif
 template <typename T> constexpr int kPartChunkT = sizeof(T) == 4 ? MVN_SA_PCHUNK_F32 : MVN_SA_PCHUNK_BF16;
 constexpr int kPartChunkMin = MVN_SA_PCHUNK_F32 < MVN_SA_PCHUNK_BF16 ? MVN_SA_PCHUNK_F32 : MVN_SA_PCHUNK_BF16;
+
+#ifndef MVN_SA_MIN_WAVES
+#define MVN_SA_MIN_WAVES 0        // >0: split the joints of pass 1 over gridDim.z below this many waves (A/B r14: no gain)
+#endif
 
 template <typename T> struct Vec;
 template <> struct Vec<float> { static constexpr int n = 4; };
@@ -156,6 +162,10 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
   constexpr int RUNS = kPartChunk / (kWave * VEC);
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const int chunk = blockIdx.x * (kSaBlock / kWave) + wid, b = blockIdx.y;
+  // joints [ja, jb) of this wave: gridDim.z splits the joints when the frames alone give too
+  // few waves to fill the chip (config 2: 8 frames x 256 chunks = 2 waves per SIMD)
+  const int jn = (J + int(gridDim.z) - 1) / int(gridDim.z), ja = int(blockIdx.z) * jn, jb = min(J, ja + jn);
+  if (ja >= jb) return;
   if (chunk >= nchunk) return;                         // whole wave; this kernel has no barriers
   const T* vb = vol + b * bstride;
   const float* cb = cub ? nullptr : coords + size_t(b) * nvox * 3;
@@ -252,7 +262,7 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
 
   const int i0 = chunk * kPartChunk + lane * VEC;
   const size_t frame_bytes = (size_t(J - 1) * size_t(jstride) + size_t(nvox)) * sizeof(T);
-  if (vec_ok && chunk * kPartChunk + kPartChunk <= nvox && J <= kWave && frame_bytes < (size_t(1) << 31) &&
+  if (vec_ok && chunk * kPartChunk + kPartChunk <= nvox && jb - ja <= kWave && frame_bytes < (size_t(1) << 31) &&
       jstride * sizeof(T) < (1u << 31)) {
     // Full chunk, aligned, frame addressable by a buffer descriptor: the raw 16-byte loads
     // of PF joints in flight (a ring of register sets refilled PF joints ahead), issued
@@ -267,7 +277,7 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
         const_cast<T*>(vb), 0, int(frame_bytes), 0x00020000);
     uint4 raw[PF][RUNS];
     auto issue = [&](int j, uint4 (&q)[RUNS]) __attribute__((always_inline)) {
-      const uint32_t jo = j < J ? uint32_t(j) * uint32_t(jstride) * uint32_t(sizeof(T)) : 0x80000000u;
+      const uint32_t jo = j < jb ? uint32_t(j) * uint32_t(jstride) * uint32_t(sizeof(T)) : 0x80000000u;
 #pragma unroll
       for (int r = 0; r < RUNS; ++r)
         q[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -285,14 +295,14 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     // analysis then merges "slot 0 issued last" into the loop: vmcnt at every ring turn)
 #pragma unroll
     for (int p = 0; p < PF; ++p) {
-      issue(p, raw[p]);
+      issue(ja + p, raw[p]);
       __builtin_amdgcn_sched_barrier(0);
     }
-    for (int j0 = 0; j0 < J; j0 += PF) {
+    for (int j0 = ja; j0 < jb; j0 += PF) {
 #pragma unroll
       for (int p = 0; p < PF; ++p) {
         const int j = j0 + p;
-        if (j >= J) goto joints_done;     // an exit edge, not a merge into the loop latch
+        if (j >= jb) goto joints_done;     // an exit edge, not a merge into the loop latch
         float x[RUNS][VEC];
 #pragma unroll
         for (int r = 0; r < RUNS; ++r) {
@@ -311,13 +321,13 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
         issue(j + PF, raw[p]);
         float q[kPartial];
         reduce_values(x, q);
-        const bool mine = lane == (j & (kWave - 1));
+        const bool mine = lane == j - ja;
 #pragma unroll
         for (int k = 0; k < kPartial; ++k) acc[k] = mine ? q[k] : acc[k];
       }
     }
   joints_done:
-    flush(0, J);
+    flush(ja, jb - ja);
     return;
   }
   if (vec_ok && chunk * kPartChunk + kPartChunk <= nvox) {
@@ -334,12 +344,12 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     };
 #pragma unroll
     for (int p = 0; p < PF; ++p)
-      if (p < J) issue(p, raw[p]);
-    for (int j0 = 0; j0 < J; j0 += PF) {
+      if (ja + p < jb) issue(ja + p, raw[p]);
+    for (int j0 = ja; j0 < jb; j0 += PF) {
 #pragma unroll
       for (int p = 0; p < PF; ++p) {
         const int j = j0 + p;
-        if (j >= J) break;
+        if (j >= jb) break;
         float x[RUNS][VEC];
 #pragma unroll
         for (int r = 0; r < RUNS; ++r) {
@@ -355,7 +365,7 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
             }
           }
         }
-        if (j + PF < J) issue(j + PF, raw[p]);
+        if (j + PF < jb) issue(j + PF, raw[p]);
         reduce_joint(j, x);
       }
     }
@@ -363,12 +373,12 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
   }
 
   float x[RUNS][VEC];
-  load(0, x);
-  for (int j = 0; j < J; ++j) {
+  load(ja, x);
+  for (int j = ja; j < jb; ++j) {
     float xn[RUNS][VEC];
-    if (j + 1 < J) load(j + 1, xn);
+    if (j + 1 < jb) load(j + 1, xn);
     reduce_joint(j, x);
-    if (j + 1 < J) {
+    if (j + 1 < jb) {
 #pragma unroll
       for (int r = 0; r < RUNS; ++r)
 #pragma unroll
@@ -451,7 +461,11 @@ int launch(const void* vol, long long bs, long long js, const float* coords, con
   const bool vec_ok = (reinterpret_cast<uintptr_t>(vol) % 16 == 0) && (bs * sizeof(T)) % 16 == 0 &&
                       (js * sizeof(T)) % 16 == 0 && (nvox % 8 == 0) &&
                       (out == nullptr || reinterpret_cast<uintptr_t>(out) % 16 == 0);
-  softargmax_partials<T, SOFTMAX><<<dim3((npart + kSaBlock / kWave - 1) / (kSaBlock / kWave), B), kSaBlock, 0, st>>>(
+  // split the joints over gridDim.z when frames x chunks give fewer than MVN_SA_MIN_WAVES
+  // pass-1 waves (4 per SIMD); each joint's partial is computed the same way either way
+  const long long waves = (long long)B * npart;
+  const int nsplit = int(std::max(1LL, std::min<long long>(J, (MVN_SA_MIN_WAVES + waves - 1) / waves)));
+  softargmax_partials<T, SOFTMAX><<<dim3((npart + kSaBlock / kWave - 1) / (kSaBlock / kWave), B, nsplit), kSaBlock, 0, st>>>(
       static_cast<const T*>(vol), bs, js, coords, cub, V, transfer, mult, part, J, nvox, npart, vec_ok);
   if (!launch_ok()) return MVN_ERR_LAUNCH;
   float* stat = part + size_t(B) * J * npart * kPartial;

@@ -287,6 +287,10 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+// Element k of a pair in both lanes.  Kept as a shuffle of the pair, the backend folds it
+// into the packed instruction's op_sel / op_sel_hi: the bilinear weights live as (w0, w1),
+// (w2, w3) pairs, 2 VGPRs per view-pair of weights instead of a {w, w} copy per weight.
+template <int K> __device__ __forceinline__ f2 splat(f2 p) { return __builtin_shufflevector(p, p, K, K); }
 
 template <typename TIn> struct ChunkT;               // 4 pixels of one channel plane
 template <> struct ChunkT<float> { using type = uint4; };

@@ -254,7 +254,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     cx = cp[0]; cy = cp[1]; cz = cp[2];
   }
   int fx[NV], fy[NV];
-  float w[NV][4];
+  f2 wp[NV][2];                        // bilinear weights (nw, ne), (sw, se) per view
   bool has[NV];
   // per-voxel geometry: footprint base pixel, bilinear weights, "samples the image" flag
   auto project_voxel = [&]() __attribute__((always_inline)) {
@@ -271,8 +271,8 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       const float fx0 = floorf(p.ix), fy0 = floorf(p.iy);
       const bool h = act & !p.invalid & (fx0 >= -1.f) & (fx0 < float(W)) & (fy0 >= -1.f) & (fy0 < float(H));
       const float tx_ = p.ix - fx0, sx_ = 1.f - tx_, ty_ = p.iy - fy0, sy_ = 1.f - ty_;
-      w[v][0] = h ? sy_ * sx_ : 0.f; w[v][1] = h ? sy_ * tx_ : 0.f;
-      w[v][2] = h ? ty_ * sx_ : 0.f; w[v][3] = h ? ty_ * tx_ : 0.f;
+      wp[v][0] = f2{h ? sy_ * sx_ : 0.f, h ? sy_ * tx_ : 0.f};
+      wp[v][1] = f2{h ? ty_ * sx_ : 0.f, h ? ty_ * tx_ : 0.f};
       fx[v] = h ? int(fx0) : 0; fy[v] = h ? int(fy0) : 0;
       has[v] = h;
     }
@@ -448,7 +448,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       const Slot bq = *reinterpret_cast<const Slot*>(buf + anw[v] + kSlotB);
       const Slot cq = *reinterpret_cast<const Slot*>(buf + asw[v]);
       const Slot d = *reinterpret_cast<const Slot*>(buf + asw[v] + kSlotB);
-      const f2 w0{w[v][0], w[v][0]}, w1{w[v][1], w[v][1]}, w2{w[v][2], w[v][2]}, w3{w[v][3], w[v][3]};
+      const f2 w0 = splat<0>(wp[v][0]), w1 = splat<1>(wp[v][0]), w2 = splat<0>(wp[v][1]), w3 = splat<1>(wp[v][1]);
       sv[0][v] = pk_fma(lo2(d), w3, pk_fma(lo2(cq), w2, pk_fma(lo2(bq), w1, lo2(a) * w0)));
       sv[1][v] = pk_fma(hi2(d), w3, pk_fma(hi2(cq), w2, pk_fma(hi2(bq), w1, hi2(a) * w0)));
       if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight

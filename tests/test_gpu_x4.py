@@ -148,3 +148,21 @@ def test_x4_partial_tiles(device, method, dt):
         assert max_rel(got, ref) <= 1e-5
     else:
         np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("dt", ("f32", "bf16"))
+def test_x4_repeat_launches_bit_identical_full_size(device, dt):
+    """Config-size volumes (4 x 32 x 96^2 -> 64^3) launched three times in each layout are
+    bit-identical, and the channels-last volume is the NCDHW one transposed.  Guards the
+    store-data hazard class (a >8-byte store whose data registers the next instruction
+    overwrites: nondeterministic channels)."""
+    from mvn_rocm import op, synth, v2v
+    dtype = torch.bfloat16 if dt == "bf16" else torch.float32
+    vb = synth.volumetric_batch(1, dtype=dtype, device=device, seed=57)
+    nc = [op.unproject_heatmaps(vb.features, vb.proj, vb.coords, "softmax") for _ in range(3)]
+    cl = [v2v.unproject_channels_last(vb.features, vb.proj, vb.coords, "softmax", out_dtype=dtype) for _ in range(3)]
+    for t in nc[1:]:
+        assert torch.equal(_bits(t), _bits(nc[0]))
+    for t in cl[1:]:
+        assert torch.equal(_bits(t), _bits(cl[0]))
+    assert torch.equal(_bits(cl[0]), _bits(nc[0].permute(0, 2, 3, 4, 1)))

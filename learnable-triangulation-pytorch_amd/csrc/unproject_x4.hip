@@ -89,9 +89,6 @@ __device__ unsigned long long g_x4_stamps[1 << 21];
 #ifndef MVN_X4_BF16_LDS
 #define MVN_X4_BF16_LDS 0           // 1: bf16 maps staged as bf16, 8-byte LDS slots of 4 channels
 #endif                              //    (bit-identical; cfg3 533 -> 570 us: the widening VALU costs more)
-#ifndef MVN_X4_TAP_PIPE
-#define MVN_X4_TAP_PIPE 0           // 1: one-view lookahead on the tap reads of the one-pass loop
-#endif
 #ifndef MVN_X4_CL_GROUPS
 #define MVN_X4_CL_GROUPS 4          // bf16 channels-last: channel groups per run of 16-byte stores (1, 2, 4)
 #endif
@@ -457,30 +454,6 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight
     }
   };
-  // One-pass form with a one-view lookahead: view v + 2's taps are read while view v is
-  // sampled (two views' taps in flight, as above, but no gap between the batches).
-  auto sample_views_pipe = [&](const char* buf, f2 (&sv)[2][NV]) __attribute__((always_inline)) {
-    Slot T[2][4];
-    auto rd = [&](int v, Slot (&q)[4]) __attribute__((always_inline)) {
-      q[0] = *reinterpret_cast<const Slot*>(buf + anw[v]);
-      q[1] = *reinterpret_cast<const Slot*>(buf + anw[v] + kSlotB);
-      q[2] = *reinterpret_cast<const Slot*>(buf + asw[v]);
-      q[3] = *reinterpret_cast<const Slot*>(buf + asw[v] + kSlotB);
-    };
-    rd(0, T[0]);
-    rd(1, T[1]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const Slot(&q)[4] = T[v & 1];
-      const f2 w0 = splat<0>(wp[v][0]), w1 = splat<1>(wp[v][0]), w2 = splat<0>(wp[v][1]), w3 = splat<1>(wp[v][1]);
-      sv[0][v] = pk_fma(lo2(q[3]), w3, pk_fma(lo2(q[2]), w2, pk_fma(lo2(q[1]), w1, lo2(q[0]) * w0)));
-      sv[1][v] = pk_fma(hi2(q[3]), w3, pk_fma(hi2(q[2]), w2, pk_fma(hi2(q[1]), w1, hi2(q[0]) * w0)));
-      __builtin_amdgcn_sched_barrier(0);
-      if (v + 2 < NV) rd(v + 2, T[v & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
   uint2 cl_buf[MVN_X4_CL_GROUPS > 1 ? MVN_X4_CL_GROUPS - 1 : 1];
 #pragma unroll
   for (int k = 0; k < (MVN_X4_CL_GROUPS > 1 ? MVN_X4_CL_GROUPS - 1 : 1); ++k) cl_buf[k] = make_uint2(0u, 0u);
@@ -578,8 +551,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
 
   auto consume = [&](const Slot* buf, int c0, float (&r)[G]) __attribute__((always_inline)) {
     f2 sv[2][NV];
-    if (MVN_X4_TAP_PIPE) sample_views_pipe(reinterpret_cast<const char*>(buf), sv);
-    else sample_views(reinterpret_cast<const char*>(buf), true, 0, sv);
+    sample_views(reinterpret_cast<const char*>(buf), true, 0, sv);
     aggregate(c0, sv, r);
     __builtin_amdgcn_sched_barrier(0);
   };

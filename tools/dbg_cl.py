@@ -1,11 +1,15 @@
+"""Debug aid (r14): bitwise comparison of the config-5-sized unprojection (bf16, 1 frame) between
+two builds of libmvn_hip.so, repeat-launch determinism of each, and channels-last vs NCDHW.
+    python tools/dbg_cl.py libA.so [libB.so]   (default: the in-tree library twice)"""
 import ctypes, os, sys
 sys.path.insert(0, "learnable-triangulation-pytorch_amd")
 import torch
 from mvn_rocm import _lib, synth
+LIBS = (sys.argv[1:] + ["learnable-triangulation-pytorch_amd/mvn_rocm/libmvn_hip.so"] * 2)[:2]
 dev = torch.device("cuda:0")
 vb = synth.volumetric_batch(1, dtype=torch.bfloat16, device=dev, seed=55)
 res = {}
-for path in ["tools/bin/defer.so", "learnable-triangulation-pytorch_amd/mvn_rocm/libmvn_hip.so"]:
+for path in LIBS:
     lib = ctypes.CDLL(os.path.abspath(path))
     for n in ("mvn_unproject_ex", "mvn_unproject"):
         if n in _lib.SIGNATURES:
@@ -25,7 +29,7 @@ if d.any():
     print("first:", idx[:10].tolist())
     print("a", a[d][:10].float().tolist()); print("b", b[d][:10].float().tolist())
 # determinism of the current build, and channels-last vs NCDHW for each build
-for path in ["tools/bin/defer.so", "learnable-triangulation-pytorch_amd/mvn_rocm/libmvn_hip.so"]:
+for path in LIBS:
     lib = ctypes.CDLL(os.path.abspath(path))
     for n in ("mvn_unproject_ex", "mvn_unproject"):
         r_, a_ = _lib.SIGNATURES[n]; getattr(lib, n).restype, getattr(lib, n).argtypes = r_, a_

@@ -51,6 +51,8 @@ def unproject(feat: Tensor, proj: Tensor, coords: Tensor, conf: Optional[Tensor]
     B, N, C, H, W = feat.shape
     Vx, Vy, Vz = coords.shape[1:4]
     out = torch.empty((B, C, Vx, Vy, Vz), dtype=_CODE_DTYPE[out_dtype], device=feat.device)
+    if out.numel() == 0:                  # empty batch: the reference returns the empty volume
+        return out
     code = _lib.load().mvn_unproject(
         feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), coords.data_ptr(), _ptr(conf),
         out.data_ptr(), out_dtype, B, N, C, H, W, Vx, Vy, Vz, agg, int(align_corners), _stream(feat))
@@ -106,6 +108,8 @@ def unproject_cuboid(feat: Tensor, proj: Tensor, cuboids: Tensor, volume_size: i
     B, N, C, H, W = feat.shape
     V = int(volume_size)
     out = torch.empty((B, C, V, V, V), dtype=_CODE_DTYPE[out_dtype], device=feat.device)
+    if out.numel() == 0:
+        return out
     code = _lib.load().mvn_unproject_cuboid(
         feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), cuboids.data_ptr(), int(transfer), _ptr(conf),
         out.data_ptr(), out_dtype, _lib.MVN_LAYOUT_NCDHW, B, N, C, H, W, V, agg, int(align_corners), _stream(feat))
@@ -182,6 +186,8 @@ def dlt(proj: Tensor, pts: Tensor, conf: Optional[Tensor]) -> Tensor:
     _require_gpu(proj, pts, conf)
     B, N, J = pts.shape[:3]
     out = torch.empty((B, J, 3), dtype=torch.float32, device=pts.device)
+    if out.numel() == 0:                  # multiview.py:164-174 on an empty batch: (0, J, 3)
+        return out
     code = _lib.load().mvn_dlt(proj.data_ptr(), pts.data_ptr(), _ptr(conf), out.data_ptr(), B, N, J,
                                _stream(pts))
     _lib.check(code, "mvn_dlt")

@@ -288,3 +288,27 @@ def test_c_abi_two_threads_two_streams(device):
         for o, x in zip(*results[i]):
             assert torch.equal(o, serial[i])
             assert torch.equal(x, ref_xyz)
+
+
+# ----------------------------------------------------------------------------- empty batches
+def test_empty_batch_matches_reference_behaviour(device):
+    """B = 0 as the reference handles it: unproject_heatmaps returns the empty (0, C, V^3)
+    volume (op.py:104-107, the batch loop never runs) and triangulate_batch_of_points the
+    empty (0, J, 3) points (multiview.py:164-174); the soft-argmaxes raise RuntimeError like the
+    reference's reshape(..., -1) of an empty tensor (op.py:16, :87)."""
+    from mvn_rocm import multiview, op, synth
+    vb = synth.volumetric_batch(1, channels=8, volume=16, seed=3)
+    feat = vb.features[:0].to(device)
+    P = vb.proj[:0].to(device)
+    coords = vb.coords[:0].to(device)
+    for method in ("sum", "softmax"):
+        out = op.unproject_heatmaps(feat, P, coords, method)
+        assert out.shape == (0, 8, 16, 16, 16) and out.dtype == torch.float32
+    ab = synth.algebraic_batch(1, 4, 17, seed=0)
+    X = multiview.triangulate_batch_of_points(ab.proj[:0].to(device), ab.points[:0].to(device),
+                                              ab.confidences[:0].to(device))
+    assert X.shape == (0, 17, 3)
+    with pytest.raises(RuntimeError):
+        op.integrate_tensor_3d_with_coordinates(torch.zeros((0, 17, 16, 16, 16), device=device), coords)
+    with pytest.raises(RuntimeError):
+        op.integrate_tensor_2d(torch.zeros((0, 17, 8, 8), device=device))

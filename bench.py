@@ -83,14 +83,22 @@ def launch_ranks(n: int) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    # poll every rank: whichever fails first (not only rank 0) ends the others, which would
+    # otherwise block in a barrier or collective that never completes
     rc = 0
-    for p in procs:
-        code = p.wait()
-        if code != 0 and rc == 0:
-            rc = code
-            for q in procs:          # one rank failed: the others would block in a collective
-                if q.poll() is None:
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
                     q.terminate()
+        if live:
+            time.sleep(0.05)
     return rc
 
 
@@ -262,13 +270,21 @@ class Workload:
         if cuboid:      # coordinates formed inside both kernels (mvn_*_cuboid), never materialised
             self.coords = vb.cuboids(device)
         self.ev = []
-        self._event = lambda: torch.cuda.Event(enable_timing=True)
+        self._pool = []
+        self.last = None
+
+    def reserve_events(self, n):
+        """Pre-create the timing events of n timed steps, so that no Event is constructed
+        inside the timed region (only recorded)."""
+        import torch
+        self._pool = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(n)]
+        self.ev = []
 
     def step(self, timed=False):
         from mvn_rocm import dist as mdist, op
         J = self.cfg["joints"]
         if timed:
-            e0, e1, e2 = self._event(), self._event(), self._event()
+            e0, e1, e2 = self._pool[len(self.ev)]
             e0.record()
         vol = op.unproject_heatmaps(self.feat, self.proj, self.coords, "softmax")
         if timed:
@@ -277,6 +293,7 @@ class Workload:
         if timed:
             e2.record()
             self.ev.append((e0, e1, e2))
+        self.last = (vol, xyz)
         if self.world > 1:      # the path's one exchange: joints of every rank, RCCL over xGMI
             xyz = mdist.gather_joints(xyz, self.global_batch)
         return xyz, sm
@@ -292,12 +309,13 @@ def run_config(name, args, rank, world, device, clock, cuboid=False, cfg=None, f
     import torch
     cfg = cfg if cfg is not None else _configs()[name]
     wl = Workload(cfg, rank, world, device, cuboid=cuboid, first_frame=first_frame)
+    wl.reserve_events(args.steps)
     elapsed = timed_loop(lambda t: wl.step(t), args, clock)
     E = 2 if cfg["dtype"] == torch.bfloat16 else 4
     frames_total = wl.global_batch * args.steps
     unproj_ms, sa_ms = wl.kernel_ms()
     launch_bytes = unproject_bytes(cfg, E, cuboid) * cfg["frames"]
-    return dict(cfg=cfg, elapsed=elapsed, fps=frames_total / elapsed, ms_per_step=elapsed / args.steps * 1e3,
+    return dict(cfg=cfg, workload=wl, elapsed=elapsed, fps=frames_total / elapsed, ms_per_step=elapsed / args.steps * 1e3,
                 unproject_ms=unproj_ms, softargmax_ms=sa_ms, launch_bytes=launch_bytes,
                 achieved_gbps=launch_bytes / (unproj_ms * 1e-3) / 1e9,
                 path_gbps=frame_bytes(cfg, E, cuboid) * frames_total / elapsed / 1e9)
@@ -447,9 +465,57 @@ def cpu_baseline(budget_s=8.0):
                 threads_1=dict(value=n_one * B / el_one, unit="frames/s", cores=1,
                                sample=f"{n_one} batch(es) of {B} frames in {el_one:.1f} s, 1 thread"),
                 host_physical_cores=phys, host_logical_cpus=logical,
+                threads_policy=(f"{threads} threads = this job's CPU share on the GPU box (the pool sets "
+                                f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', '?')} per GPU and asks jobs "
+                                f"not to exceed it); SURVEY.md §8d's os.cpu_count() ({logical}) counts the whole "
+                                f"shared host, which this job may not occupy"),
                 config1_dlt_ms_per_frame=dlt_ms,
                 config1_sample=f"{nd} calls of restate_torch.triangulate_batch_of_points (multiview.py:132-174), "
                                f"batch 1, 4 views x 17 joints, {threads} threads")
+
+
+def parity_check(res):
+    """Parity of the timed workload itself (SURVEY.md §5 'Metrics': the line carries the parity
+    error): frame 0 of the last timed step's unprojection and joints against the C oracle
+    (oracle/mvn_oracle.c, pinned to the reference's goldens) on the same inputs.
+      unproject_max_rel    GPU volume vs oracle unproject_heatmaps (op.py:99-163), softmax agg;
+                           max|d| / max|ref| over the frame's C x 64^3 values
+      joints_max_rel       GPU joints vs the oracle soft-argmax (op.py:84-96) of the GPU's own
+                           channels [0:17] (the same input the GPU's soft-argmax saw)
+      chain_joints_max_rel GPU joints vs the oracle chain unproject -> soft-argmax end to end
+    bf16 maps: the oracle runs in f32 on the same bf16 bits; the GPU writes a bf16 volume."""
+    import numpy as np
+    import torch
+    from oracle import capi
+    wl = res["workload"]
+    vol, xyz = wl.last
+    J = wl.cfg["joints"]
+    bf16 = wl.feat.dtype == torch.bfloat16
+    feat = wl.feat[:1].cpu()
+    feat = feat.view(torch.int16).numpy().view(np.uint16) if bf16 else feat.numpy()
+    proj, coords = wl.proj[:1].cpu().numpy(), wl.coords[:1].cpu().numpy()
+    t0 = time.perf_counter()
+    ref_vol = capi.unproject(feat, proj, coords, "softmax", feat_bf16_bits=bf16)
+    got_vol = vol[:1].float().cpu().numpy()
+    got_xyz = xyz[:1].cpu().numpy().astype(np.float64)
+    own_xyz, _ = capi.softargmax3d(np.ascontiguousarray(got_vol[:, :J]), coords, True, 1.0)
+    ref_xyz, _ = capi.softargmax3d(np.ascontiguousarray(ref_vol[:, :J]), coords, True, 1.0)
+
+    def rel(a, b):
+        return float(np.abs(a.astype(np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+    out = {}
+    if vol.dtype == torch.bfloat16:
+        # bf16 volume: every value within one bf16 ulp of the f32 oracle (+ the softmax's 1e-5
+        # f32 tolerance, where the aggregate cancels towards 0)
+        _, e = np.frexp(ref_vol.astype(np.float64))
+        ulp = np.where(ref_vol == 0, 0.0, np.ldexp(1.0, e - 8))
+        out["unproject_within_one_bf16_ulp"] = bool(
+            (np.abs(got_vol.astype(np.float64) - ref_vol) <= ulp + 1e-5 * np.abs(ref_vol).max()).all())
+    return dict(out, unproject_max_rel=rel(got_vol, ref_vol), joints_max_rel=rel(got_xyz, own_xyz),
+                chain_joints_max_rel=rel(got_xyz, ref_xyz), frames_checked=1,
+                bars="unproject <= 1e-5 (f32 out) / one bf16 ulp (bf16 out); joints <= 1e-4 (north_star)",
+                oracle="oracle/mvn_oracle.c via oracle/capi.py", oracle_s=time.perf_counter() - t0)
 
 
 # ----------------------------------------------------------------------------- dry run (CPU)
@@ -498,6 +564,8 @@ def main():
     ap.add_argument("--no-in-kernel-coords", action="store_true",
                     help="skip the in-kernel-coordinates run (keeps rocprof kernel means per variant clean)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo protocol check, no GPU")
+    ap.add_argument("--dry-run-fail-rank", type=int, default=-1,
+                    help="(tests) this rank of a dry run exits with an error before its first barrier")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -515,6 +583,8 @@ def main():
     if args.dry_run:
         if world > 1:
             dist.init_process_group("gloo")
+        if rank == args.dry_run_fail_rank:
+            raise SystemExit(f"rank {rank}: failing on request (--dry-run-fail-rank)")
         line = dry_run(args, rank, world)
         if rank == 0:
             print(json.dumps(line), flush=True)
@@ -532,9 +602,9 @@ def main():
     extras = not args.no_secondary and args.config == "2"
 
     main_res = run_config(args.config, args, rank, world, device, clock)
-    secondary = config1 = in_kernel_coords = cfg4 = cfg5 = None
+    secondary = config1 = in_kernel_coords = cfg4 = cfg5 = sec_res = None
     if extras:
-        s = run_config("3", args, rank, world, device, clock)
+        s = sec_res = run_config("3", args, rank, world, device, clock)
         secondary = dict(workload=s["cfg"]["label"], value=s["fps"], unit="frames/s", ms_per_step=s["ms_per_step"],
                          frames_per_gpu=s["cfg"]["frames"], dtype="bf16", unproject_ms=s["unproject_ms"],
                          softargmax_ms=s["softargmax_ms"], roofline=roofline(s["cfg"], s, "3", device),
@@ -567,9 +637,14 @@ def main():
             cfg5["in_kernel_coords"] = dict(value=k5["value"], unit="frames/s", ms_per_step=k5["ms_per_step"])
         if rank == 0:
             config1 = run_config1(args, device)
-    base = None
+    base = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the CPU leg: the reference algorithm timed on the host, and the timed workloads'
+        # outputs checked against the oracle (never inside a timed region)
         base = cpu_baseline()
+        parity = parity_check(main_res)
+        if secondary is not None:
+            secondary["parity"] = parity_check(sec_res)
 
     if rank == 0:
         r, c = main_res, main_res["cfg"]
@@ -596,6 +671,7 @@ def main():
             "path_algorithmic_gbps": r["path_gbps"],
             "path_frac": r["path_gbps"] / HBM_PEAK_GBPS,
             "cpu_baseline": base,
+            "parity": parity,
             "secondary": secondary,
             "config1": config1,
             "in_kernel_coords": in_kernel_coords,

@@ -163,7 +163,9 @@ int mvn_v2v_front(const void* vol_cl, const void* weight_packed, const float* sc
  * default, one group's intermediate within half of the 256 MiB MALL: 8 frames at V = 64)
  * through `workspace` (>= mvn_unproject_v2v_front_workspace_bytes(group_frames, V) bytes).
  * Replaces triangulation.py:349-352 up to V2VModel.front_layers[0] (v2v.py:145-146).
- *   C == 32, V % 16 == 0, agg != MVN_AGG_CONF; exactly one of coords / cuboids non-NULL.
+ *   C == 32, V % 16 == 0, agg != MVN_AGG_CONF, 1 <= N <= 8 views (the channels-last
+ *   kernels), B >= 1 (MVN_ERR_SHAPE otherwise; mvn_rocm.v2v.unproject_v2v_front routes more
+ *   views and empty batches through the two calls); exactly one of coords / cuboids non-NULL.
  *   out (B, 16, V, V, V) out_dtype.  Bit-identical to the two calls on the whole batch.
  */
 size_t mvn_unproject_v2v_front_workspace_bytes(int group_frames, int V);
@@ -248,6 +250,23 @@ int mvn_unproject_backward(const void* feat, int feat_dtype, const float* proj, 
                            float* grad_feat, float* grad_conf,
                            int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
                            int agg, int align_corners, void* stream);
+
+/*
+ * Deterministic variant of mvn_unproject_backward (the reference trains under
+ * autograd.detect_anomaly, train.py:178; torch.use_deterministic_algorithms(True) selects
+ * this in mvn_rocm): every contribution is accumulated as a 64-bit fixed-point integer with
+ * 32 fraction bits (integer adds are associative), then converted to f32 — two runs are
+ * bit-identical.  Range |sum| < 2^31, absolute resolution 2^-32 per contribution.
+ *   workspace  >= mvn_unproject_backward_workspace_bytes(B, N, C, H, W) bytes, any content
+ *   grad_feat / grad_conf are fully written (no zero-initialisation needed).
+ */
+size_t mvn_unproject_backward_workspace_bytes(int B, int N, int C, int H, int W);
+int mvn_unproject_backward_deterministic(const void* feat, int feat_dtype, const float* proj,
+                                         const float* coords, const float* conf, const void* grad_out,
+                                         int grad_out_dtype, float* grad_feat, float* grad_conf,
+                                         void* workspace, size_t workspace_bytes,
+                                         int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+                                         int agg, int align_corners, void* stream);
 
 /*
  * d/d(vol) of mvn_softargmax3d (vol as passed to the forward, i.e. before `multiplier`).

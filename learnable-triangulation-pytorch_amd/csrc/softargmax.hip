@@ -276,12 +276,16 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<T*>(vb), 0, int(frame_bytes), 0x00020000);
     uint4 raw[PF][RUNS];
+    // past the last joint the out-of-range marker rides in the per-lane offset (voffset, which
+    // the range check always covers: frame_bytes < 2^31), soffset 0 — the load returns zeros
+    // without a memory access
     auto issue = [&](int j, uint4 (&q)[RUNS]) __attribute__((always_inline)) {
-      const uint32_t jo = j < jb ? uint32_t(j) * uint32_t(jstride) * uint32_t(sizeof(T)) : 0x80000000u;
+      const bool live = j < jb;
+      const uint32_t jo = live ? uint32_t(j) * uint32_t(jstride) * uint32_t(sizeof(T)) : 0u;
 #pragma unroll
       for (int r = 0; r < RUNS; ++r)
         q[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             vrs, uint32_t((i0 + r * kWave * VEC) * sizeof(T)), jo, 0));
+                                             vrs, live ? uint32_t((i0 + r * kWave * VEC) * sizeof(T)) : 0x80000000u, jo, 0));
     };
     float acc[kPartial] = {0.f, 0.f, 0.f, 0.f, 0.f};
     auto flush = [&](int jbase, int n) __attribute__((always_inline)) {

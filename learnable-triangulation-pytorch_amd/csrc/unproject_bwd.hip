@@ -18,6 +18,16 @@
 // it with one global float atomic per touched (pixel, channel) — ~10x fewer global atomics
 // than scattering every tap.  Float atomics make the result order-nondeterministic in the
 // last bits (documented in DESIGN.md).
+//
+// Deterministic mode (DET; mvn_unproject_backward_deterministic, selected by the Python layer
+// under torch.use_deterministic_algorithms(True)): every contribution — the same f32 product
+// as above — is quantised to a 64-bit fixed-point integer with 32 fraction bits, and both
+// the LDS and the global accumulation are integer adds (ds_add_u64 / global_atomic_add_x2),
+// which are associative: the sums do not depend on the order the waves and blocks arrive
+// in, so two runs are bit-identical.  A last kernel converts the integers back to f32.
+// Contract of the mode: |gradient sums| < 2^31, absolute resolution 2^-32 per contribution.
+#include <algorithm>
+
 #include "unproject_common.hpp"
 
 namespace mvn {
@@ -33,17 +43,34 @@ constexpr int TX = 4, TY = 8, TZ = 8;        // one voxel per thread
 
 template <typename T> __device__ __forceinline__ float ldf(const T* p, size_t i) { return to_f32(p[i]); }
 
-template <int AGG, typename TIn, typename TG, int NV>
+// deterministic mode: f32 contribution -> 32.32 fixed point (round to nearest; clamped far
+// outside the mode's range so the conversion is defined)
+constexpr float kFix = 4294967296.f;           // 2^32
+__device__ __forceinline__ unsigned long long to_fix(float x) {
+  const float y = fminf(fmaxf(x * kFix, -0x1p62f), 0x1p62f);
+  return static_cast<unsigned long long>(__float2ll_rn(y));
+}
+// float accumulate (default) or fixed-point accumulate (DET) into a global element
+template <bool DET>
+__device__ __forceinline__ void global_add(float* f, unsigned long long* q, size_t i, float x) {
+  if constexpr (DET) atomicAdd(q + i, to_fix(x));
+  else atomicAdd(f + i, x);
+}
+
+template <int AGG, typename TIn, typename TG, int NV, bool DET>
 __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ conf, const TG* __restrict__ gout, float* __restrict__ gfeat,
-    float* __restrict__ gconf, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners) {
+    float* __restrict__ gconf, unsigned long long* __restrict__ qfeat, unsigned long long* __restrict__ qconf,
+    int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners) {
   constexpr bool kNeedSamples = AGG == MVN_AGG_SOFTMAX || AGG == MVN_AGG_MAX || AGG == MVN_AGG_CONF;
   __shared__ float4 fstage[kSlots];          // forward features (channels-last)
-  __shared__ float4 gacc[kSlots];            // gradient accumulator (channels-last)
+  __shared__ float4 gacc[DET ? 1 : kSlots];  // gradient accumulator (channels-last)
+  __shared__ unsigned long long gq[DET ? kSlots * G : 1];   // the same in 32.32 fixed point (DET)
   __shared__ int red[kWaves][NV][4];
   __shared__ int region[NV][5];              // xs, ys, bw, pitch, base
   __shared__ float gconf_acc[NV][G];
+  __shared__ unsigned long long gconf_q[DET ? NV : 1][G];
   __shared__ int info[2];                    // total slots (or -1: direct global path)
 
   const int nTx = (Vx + TX - 1) / TX, nTy = (Vy + TY - 1) / TY, nTz = (Vz + TZ - 1) / TZ;
@@ -61,7 +88,7 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
   const float cx = cp[0], cy = cp[1], cz = cp[2];
   const float* Pb = P + size_t(b) * N * 12;
   const TIn* fb = feat + size_t(b) * N * C * HW;
-  float* gfb = gfeat + size_t(b) * N * C * HW;
+  const size_t fbo = size_t(b) * N * C * HW;   // this frame's first element of grad_feat
 
   if (t < 2) { fstage[kZero + t] = make_float4(0.f, 0.f, 0.f, 0.f); }
 
@@ -151,14 +178,14 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
         else if constexpr (AGG == MVN_AGG_MAX) coef[v] = v == arg ? g : 0.f;
         else coef[v] = g * (softmax_exp(s[v], m * kLog2e) * __builtin_amdgcn_rcpf(den)) * (1.f + s[v] - out);
         if (coef[v] != 0.f) {
-          float* pl = gfb + (size_t(v) * C + c) * HW;
-          if (tp[v].w0 != 0.f) atomicAdd(pl + tp[v].o0, coef[v] * tp[v].w0);
-          if (tp[v].w1 != 0.f) atomicAdd(pl + tp[v].o1, coef[v] * tp[v].w1);
-          if (tp[v].w2 != 0.f) atomicAdd(pl + tp[v].o2, coef[v] * tp[v].w2);
-          if (tp[v].w3 != 0.f) atomicAdd(pl + tp[v].o3, coef[v] * tp[v].w3);
+          const size_t pl = fbo + (size_t(v) * C + c) * HW;
+          if (tp[v].w0 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o0, coef[v] * tp[v].w0);
+          if (tp[v].w1 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o1, coef[v] * tp[v].w1);
+          if (tp[v].w2 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o2, coef[v] * tp[v].w2);
+          if (tp[v].w3 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o3, coef[v] * tp[v].w3);
         }
         if constexpr (AGG == MVN_AGG_CONF)
-          if (gconf && v < N && g * s[v] != 0.f) atomicAdd(gconf + (size_t(b) * N + v) * C + c, g * s[v]);
+          if (gconf && v < N && g * s[v] != 0.f) global_add<DET>(gconf, qconf, (size_t(b) * N + v) * C + c, g * s[v]);
       }
     }
     return;
@@ -180,7 +207,12 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
   for (int c0 = 0; c0 < C; c0 += G) {
     // ---- zero the accumulator, stage forward features ---------------------------------
     for (int idx = t; idx < total; idx += kThreads) {
-      gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (DET) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) gq[idx * G + k] = 0ull;
+      } else {
+        gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
       if constexpr (kNeedSamples) {
         int v = 0;
 #pragma unroll
@@ -198,7 +230,10 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
         fstage[idx] = make_float4(q[0], q[1], q[2], q[3]);
       }
     }
-    if (t < NV * G) gconf_acc[t / G][t % G] = 0.f;
+    if (t < NV * G) {
+      if constexpr (DET) gconf_q[t / G][t % G] = 0ull;
+      else gconf_acc[t / G][t % G] = 0.f;
+    }
     __syncthreads();
 
     // ---- per voxel: samples, upstream gradient, d agg / d s_v, LDS scatter ------------
@@ -253,12 +288,21 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         if (v >= N || !has[v] || coef[v] == 0.f) continue;
-        float* base0 = reinterpret_cast<float*>(&gacc[slot[v]]) + k;
-        float* base1 = reinterpret_cast<float*>(&gacc[slot[v] + rpitch[v]]) + k;
-        atomicAdd(base0, coef[v] * w[v][0]);
-        atomicAdd(base0 + 4, coef[v] * w[v][1]);
-        atomicAdd(base1, coef[v] * w[v][2]);
-        atomicAdd(base1 + 4, coef[v] * w[v][3]);
+        if constexpr (DET) {
+          unsigned long long* q0 = &gq[slot[v] * G + k];
+          unsigned long long* q1 = &gq[(slot[v] + rpitch[v]) * G + k];
+          atomicAdd(q0, to_fix(coef[v] * w[v][0]));
+          atomicAdd(q0 + G, to_fix(coef[v] * w[v][1]));
+          atomicAdd(q1, to_fix(coef[v] * w[v][2]));
+          atomicAdd(q1 + G, to_fix(coef[v] * w[v][3]));
+        } else {
+          float* base0 = reinterpret_cast<float*>(&gacc[slot[v]]) + k;
+          float* base1 = reinterpret_cast<float*>(&gacc[slot[v] + rpitch[v]]) + k;
+          atomicAdd(base0, coef[v] * w[v][0]);
+          atomicAdd(base0 + 4, coef[v] * w[v][1]);
+          atomicAdd(base1, coef[v] * w[v][2]);
+          atomicAdd(base1 + 4, coef[v] * w[v][3]);
+        }
       }
       if constexpr (AGG == MVN_AGG_CONF) {
         if (gconf) {
@@ -268,7 +312,10 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
             float part = g[k] * s[v][k];
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
-            if (lane == 0 && part != 0.f) atomicAdd(&gconf_acc[v][k], part);
+            if (lane == 0 && part != 0.f) {
+              if constexpr (DET) atomicAdd(&gconf_q[v][k], to_fix(part));
+              else atomicAdd(&gconf_acc[v][k], part);
+            }
           }
         }
       }
@@ -286,50 +333,111 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
       const int py = (idx - base) / pv, px = idx - base - py * pv;
       const int gx = xs + px, gy = ys + py;
       if ((px < bwv) & (gx >= 0) & (gx < W) & (gy >= 0) & (gy < H)) {
-        const float4 a = gacc[idx];
-        const float av[4] = {a.x, a.y, a.z, a.w};
+        const size_t pix = fbo + size_t(gy) * W + gx;
+        if constexpr (DET) {
 #pragma unroll
-        for (int k = 0; k < G; ++k)
-          if (c0 + k < C && av[k] != 0.f) atomicAdd(gfb + (size_t(v) * C + c0 + k) * HW + size_t(gy) * W + gx, av[k]);
+          for (int k = 0; k < G; ++k) {
+            const unsigned long long q = gq[idx * G + k];
+            if (c0 + k < C && q != 0ull) atomicAdd(qfeat + pix + (size_t(v) * C + c0 + k) * HW, q);
+          }
+        } else {
+          const float4 a = gacc[idx];
+          const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+          for (int k = 0; k < G; ++k)
+            if (c0 + k < C && av[k] != 0.f) atomicAdd(gfeat + pix + (size_t(v) * C + c0 + k) * HW, av[k]);
+        }
       }
     }
     if constexpr (AGG == MVN_AGG_CONF) {
       if (gconf && t < NV * G) {
         const int v = t / G, k = t % G;
-        if (v < N && c0 + k < C && gconf_acc[v][k] != 0.f) atomicAdd(gconf + (size_t(b) * N + v) * C + c0 + k, gconf_acc[v][k]);
+        const size_t o = (size_t(b) * N + v) * C + c0 + k;
+        if constexpr (DET) {
+          if (v < N && c0 + k < C && gconf_q[v][k] != 0ull) atomicAdd(qconf + o, gconf_q[v][k]);
+        } else {
+          if (v < N && c0 + k < C && gconf_acc[v][k] != 0.f) atomicAdd(gconf + o, gconf_acc[v][k]);
+        }
       }
     }
     __syncthreads();
   }
 }
 
-template <int AGG, typename TIn, typename TG>
+// fixed-point sums (DET) -> f32 gradients
+__global__ void fix_to_f32(const unsigned long long* __restrict__ q, float* __restrict__ out, size_t n) {
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+    out[i] = float(double(static_cast<long long>(q[i])) * 0x1p-32);
+}
+
+template <int AGG, typename TIn, typename TG, bool DET>
 int launch_bwd(const void* feat, const float* P, const float* coords, const float* conf, const void* gout, float* gfeat,
-               float* gconf, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int ac, hipStream_t s) {
+               float* gconf, unsigned long long* qfeat, unsigned long long* qconf, int B, int N, int C, int H, int W,
+               int Vx, int Vy, int Vz, int ac, hipStream_t s) {
   const long long nb = (long long)B * ((Vx + TX - 1) / TX) * ((Vy + TY - 1) / TY) * ((Vz + TZ - 1) / TZ);
   if (nb > INT_MAX) return MVN_ERR_SHAPE;
   if (N <= 4)
-    unproject_bwd_tiled<AGG, TIn, TG, 4><<<int(nb), kThreads, 0, s>>>(static_cast<const TIn*>(feat), P, coords, conf,
-        static_cast<const TG*>(gout), gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac);
+    unproject_bwd_tiled<AGG, TIn, TG, 4, DET><<<int(nb), kThreads, 0, s>>>(static_cast<const TIn*>(feat), P, coords,
+        conf, static_cast<const TG*>(gout), gfeat, gconf, qfeat, qconf, B, N, C, H, W, Vx, Vy, Vz, ac);
   else if (N <= 8)
-    unproject_bwd_tiled<AGG, TIn, TG, 8><<<int(nb), kThreads, 0, s>>>(static_cast<const TIn*>(feat), P, coords, conf,
-        static_cast<const TG*>(gout), gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac);
+    unproject_bwd_tiled<AGG, TIn, TG, 8, DET><<<int(nb), kThreads, 0, s>>>(static_cast<const TIn*>(feat), P, coords,
+        conf, static_cast<const TG*>(gout), gfeat, gconf, qfeat, qconf, B, N, C, H, W, Vx, Vy, Vz, ac);
   else
     return MVN_ERR_SHAPE;
   return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
 }
 
-template <typename TIn, typename TG>
+template <typename TIn, typename TG, bool DET>
 int dispatch_bwd(int agg, const void* feat, const float* P, const float* coords, const float* conf, const void* gout,
-                 float* gfeat, float* gconf, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int ac,
-                 hipStream_t s) {
+                 float* gfeat, float* gconf, unsigned long long* qfeat, unsigned long long* qconf, int B, int N, int C,
+                 int H, int W, int Vx, int Vy, int Vz, int ac, hipStream_t s) {
   switch (agg) {
-    case MVN_AGG_SUM: return launch_bwd<MVN_AGG_SUM, TIn, TG>(feat, P, coords, conf, gout, gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac, s);
-    case MVN_AGG_MAX: return launch_bwd<MVN_AGG_MAX, TIn, TG>(feat, P, coords, conf, gout, gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac, s);
-    case MVN_AGG_SOFTMAX: return launch_bwd<MVN_AGG_SOFTMAX, TIn, TG>(feat, P, coords, conf, gout, gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac, s);
-    case MVN_AGG_CONF: return launch_bwd<MVN_AGG_CONF, TIn, TG>(feat, P, coords, conf, gout, gfeat, gconf, B, N, C, H, W, Vx, Vy, Vz, ac, s);
+    case MVN_AGG_SUM:
+      return launch_bwd<MVN_AGG_SUM, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, B, N, C, H,
+                                                   W, Vx, Vy, Vz, ac, s);
+    case MVN_AGG_MAX:
+      return launch_bwd<MVN_AGG_MAX, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, B, N, C, H,
+                                                   W, Vx, Vy, Vz, ac, s);
+    case MVN_AGG_SOFTMAX:
+      return launch_bwd<MVN_AGG_SOFTMAX, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, B, N,
+                                                       C, H, W, Vx, Vy, Vz, ac, s);
+    case MVN_AGG_CONF:
+      return launch_bwd<MVN_AGG_CONF, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, B, N, C,
+                                                    H, W, Vx, Vy, Vz, ac, s);
   }
   return MVN_ERR_ARG;
+}
+
+template <bool DET>
+int backward_entry(const void* feat, int feat_dtype, const float* proj, const float* coords, const float* conf,
+                   const void* grad_out, int grad_out_dtype, float* grad_feat, float* grad_conf,
+                   unsigned long long* qfeat, unsigned long long* qconf, int B, int N, int C, int H, int W, int Vx,
+                   int Vy, int Vz, int agg, int align_corners, hipStream_t s) {
+  const bool f16 = feat_dtype == MVN_DTYPE_BF16, g16 = grad_out_dtype == MVN_DTYPE_BF16;
+  if ((feat_dtype != MVN_DTYPE_F32 && !f16) || (grad_out_dtype != MVN_DTYPE_F32 && !g16)) return MVN_ERR_DTYPE;
+  if (!f16 && !g16)
+    return dispatch_bwd<float, float, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat, qconf,
+                                           B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+  if (f16 && g16)
+    return dispatch_bwd<uint16_t, uint16_t, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat,
+                                                 qconf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+  if (f16)
+    return dispatch_bwd<uint16_t, float, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat,
+                                              qconf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+  return dispatch_bwd<float, uint16_t, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat, qconf,
+                                            B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+}
+
+int check_bwd_args(const void* feat, const float* proj, const float* coords, const float* conf, const void* grad_out,
+                   const float* grad_feat, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int agg,
+                   int align_corners) {
+  if (!feat || !proj || !coords || !grad_out || !grad_feat) return MVN_ERR_ARG;
+  if (agg < MVN_AGG_SUM || agg > MVN_AGG_CONF) return MVN_ERR_ARG;
+  if (agg == MVN_AGG_CONF && !conf) return MVN_ERR_ARG;
+  if (align_corners != 0 && align_corners != 1) return MVN_ERR_ARG;
+  if (B <= 0 || N <= 0 || C <= 0 || H <= 0 || W <= 0 || Vx <= 0 || Vy <= 0 || Vz <= 0) return MVN_ERR_SHAPE;
+  if ((long long)Vx * Vy * Vz > (1LL << 30) || (long long)H * W > (1LL << 30) || N > 8) return MVN_ERR_SHAPE;
+  return MVN_OK;
 }
 
 }  // namespace
@@ -341,18 +449,44 @@ extern "C" int mvn_unproject_backward(const void* feat, int feat_dtype, const fl
                                       float* grad_conf, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
                                       int agg, int align_corners, void* stream) {
   using namespace mvn;
-  if (!feat || !proj || !coords || !grad_out || !grad_feat) return MVN_ERR_ARG;
-  if (agg < MVN_AGG_SUM || agg > MVN_AGG_CONF) return MVN_ERR_ARG;
-  if (agg == MVN_AGG_CONF && !conf) return MVN_ERR_ARG;
-  if (align_corners != 0 && align_corners != 1) return MVN_ERR_ARG;
-  if (B <= 0 || N <= 0 || C <= 0 || H <= 0 || W <= 0 || Vx <= 0 || Vy <= 0 || Vz <= 0) return MVN_ERR_SHAPE;
-  if ((long long)Vx * Vy * Vz > (1LL << 30) || (long long)H * W > (1LL << 30) || N > 8) return MVN_ERR_SHAPE;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const bool f16 = feat_dtype == MVN_DTYPE_BF16, g16 = grad_out_dtype == MVN_DTYPE_BF16;
-  if ((feat_dtype != MVN_DTYPE_F32 && !f16) || (grad_out_dtype != MVN_DTYPE_F32 && !g16)) return MVN_ERR_DTYPE;
   using namespace mvn::unproj;
-  if (!f16 && !g16) return dispatch_bwd<float, float>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
-  if (f16 && g16) return dispatch_bwd<uint16_t, uint16_t>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
-  if (f16) return dispatch_bwd<uint16_t, float>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
-  return dispatch_bwd<float, uint16_t>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+  const int e = check_bwd_args(feat, proj, coords, conf, grad_out, grad_feat, B, N, C, H, W, Vx, Vy, Vz, agg,
+                               align_corners);
+  if (e != MVN_OK) return e;
+  return backward_entry<false>(feat, feat_dtype, proj, coords, conf, grad_out, grad_out_dtype, grad_feat, grad_conf,
+                               nullptr, nullptr, B, N, C, H, W, Vx, Vy, Vz, agg, align_corners,
+                               static_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t mvn_unproject_backward_workspace_bytes(int B, int N, int C, int H, int W) {
+  if (B <= 0 || N <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+  return (size_t(B) * N * C * size_t(H) * W + size_t(B) * N * C) * sizeof(unsigned long long);
+}
+
+extern "C" int mvn_unproject_backward_deterministic(const void* feat, int feat_dtype, const float* proj,
+                                                    const float* coords, const float* conf, const void* grad_out,
+                                                    int grad_out_dtype, float* grad_feat, float* grad_conf,
+                                                    void* workspace, size_t workspace_bytes, int B, int N, int C,
+                                                    int H, int W, int Vx, int Vy, int Vz, int agg, int align_corners,
+                                                    void* stream) {
+  using namespace mvn;
+  using namespace mvn::unproj;
+  const int e = check_bwd_args(feat, proj, coords, conf, grad_out, grad_feat, B, N, C, H, W, Vx, Vy, Vz, agg,
+                               align_corners);
+  if (e != MVN_OK) return e;
+  const size_t nfeat = size_t(B) * N * C * size_t(H) * W, nconf = size_t(B) * N * C;
+  if (!workspace || workspace_bytes < mvn_unproject_backward_workspace_bytes(B, N, C, H, W)) return MVN_ERR_WORKSPACE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto* qfeat = static_cast<unsigned long long*>(workspace);
+  auto* qconf = qfeat + nfeat;
+  if (hipMemsetAsync(workspace, 0, (nfeat + nconf) * sizeof(unsigned long long), s) != hipSuccess)
+    return MVN_ERR_LAUNCH;
+  const int r = backward_entry<true>(feat, feat_dtype, proj, coords, conf, grad_out, grad_out_dtype, grad_feat,
+                                     grad_conf, qfeat, grad_conf ? qconf : nullptr, B, N, C, H, W, Vx, Vy, Vz, agg,
+                                     align_corners, s);
+  if (r != MVN_OK) return r;
+  const int nblk = int(std::min<size_t>((nfeat + 255) / 256, 65536));
+  fix_to_f32<<<nblk, 256, 0, s>>>(qfeat, grad_feat, nfeat);
+  if (grad_conf) fix_to_f32<<<int(std::min<size_t>((nconf + 255) / 256, 65536)), 256, 0, s>>>(qconf, grad_conf, nconf);
+  return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
 }

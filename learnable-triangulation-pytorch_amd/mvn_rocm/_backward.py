@@ -28,7 +28,23 @@ def unproject_bwd(feat: Tensor, proj: Tensor, coords: Tensor, conf: Optional[Ten
         g = g.float()
     gfeat = torch.zeros((B, N, C, H, W), dtype=torch.float32, device=feat.device)
     gconf = torch.zeros((B, N, C) if want_conf else (0,), dtype=torch.float32, device=feat.device)
-    code = _lib.load().mvn_unproject_backward(
+    if feat.numel() == 0 or coords.numel() == 0:
+        # empty batch / volume / maps: the reference's autograd returns zero-sized (or zero)
+        # gradients; the forward launched nothing either (ops return the empty volume)
+        return [gfeat.to(feat.dtype), gconf]
+    lib = _lib.load()
+    if torch.are_deterministic_algorithms_enabled():
+        # torch.use_deterministic_algorithms(True): fixed-point accumulation, bit-identical
+        # across runs (mvn_unproject_backward_deterministic)
+        ws = torch.empty(lib.mvn_unproject_backward_workspace_bytes(B, N, C, H, W), dtype=torch.uint8,
+                         device=feat.device)
+        code = lib.mvn_unproject_backward_deterministic(
+            feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), coords.data_ptr(), _ptr(conf), g.data_ptr(),
+            _DTYPE_CODE[g.dtype], gfeat.data_ptr(), gconf.data_ptr() if want_conf else None, ws.data_ptr(),
+            ws.numel(), B, N, C, H, W, Vx, Vy, Vz, agg, int(align_corners), _stream(feat))
+        _lib.check(code, "mvn_unproject_backward_deterministic")
+        return [gfeat.to(feat.dtype), gconf]
+    code = lib.mvn_unproject_backward(
         feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), coords.data_ptr(), _ptr(conf), g.data_ptr(),
         _DTYPE_CODE[g.dtype], gfeat.data_ptr(), gconf.data_ptr() if want_conf else None, B, N, C, H, W, Vx, Vy, Vz,
         agg, int(align_corners), _stream(feat))
@@ -77,6 +93,8 @@ def dlt_bwd(proj: Tensor, pts: Tensor, conf: Optional[Tensor], grad_out: Tensor)
     g = grad_out.float().contiguous()
     gpts = torch.empty_like(pts)
     gconf = torch.empty((B, N, J) if conf is not None else (0,), dtype=torch.float32, device=pts.device)
+    if pts.numel() == 0:                   # empty batch: zero-sized gradients, as the reference's autograd
+        return [gpts, gconf]
     code = _lib.load().mvn_dlt_backward(proj.data_ptr(), pts.data_ptr(), _ptr(conf), g.data_ptr(), gpts.data_ptr(),
                                         gconf.data_ptr() if conf is not None else None, B, N, J, _stream(pts))
     _lib.check(code, "mvn_dlt_backward")

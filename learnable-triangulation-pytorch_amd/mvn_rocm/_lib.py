@@ -51,6 +51,10 @@ SIGNATURES = {
     "mvn_v2v_front": (_c_int, [_c_void_p] * 5 + [_c_int, _c_int, _c_int, _c_void_p]),
     "mvn_unproject_backward": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int,
                                         _c_void_p, _c_void_p] + [_c_int] * 8 + [_c_int, _c_int, _c_void_p]),
+    "mvn_unproject_backward_workspace_bytes": (_c_size_t, [_c_int] * 5),
+    "mvn_unproject_backward_deterministic": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                                      _c_int, _c_void_p, _c_void_p, _c_void_p, _c_size_t]
+                                             + [_c_int] * 8 + [_c_int, _c_int, _c_void_p]),
     "mvn_softargmax3d_backward_workspace_bytes": (_c_size_t, [_c_int] * 5),
     "mvn_softargmax3d_backward": (_c_int, [_c_void_p, _c_int, _c_i64, _c_i64, _c_void_p, _c_float, _c_int,
                                            _c_void_p, _c_void_p, _c_int, _c_void_p, _c_int, _c_void_p, _c_size_t]

@@ -53,6 +53,8 @@ def v2v_front(vol_cl, packed, scale, shift, out_dtype=torch.float32):
     _require_gpu(x, packed, scale, shift)
     od = _dtype_code(out_dtype)
     out = torch.empty((B, COUT, V, V, V), dtype=out_dtype, device=x.device)
+    if out.numel() == 0:                  # empty batch: nothing to launch
+        return out
     code = _lib.load().mvn_v2v_front(x.data_ptr(), packed.data_ptr(), scale.data_ptr(), shift.data_ptr(),
                                      out.data_ptr(), od, B, V, _stream(x))
     _lib.check(code, "mvn_v2v_front")
@@ -71,25 +73,34 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
     feat, proj, _ = unproject_inputs(heatmaps, proj_matricies, None, agg, volume_aggregation_method, cub)
     fd, od = _dtype_code(feat.dtype), _dtype_code(out_dtype)
     B, N, C, H, W = feat.shape
-    if cub is not None and N <= 8:
+    if N > 8:
+        # the channels-last kernels take N <= 8 views (mvn_hip.h): more views go through the
+        # NCDHW unprojection (any N) and one permute on the device
+        from .op import unproject_heatmaps
+        vol = unproject_heatmaps(feat, proj, coord_volumes, volume_aggregation_method, align_corners=align_corners)
+        # f32 -> bf16 rounds to nearest even, as the kernels' own bf16 stores do
+        return vol.permute(0, 2, 3, 4, 1).to(out_dtype).contiguous()
+    if cub is not None:
         # coordinates formed in-kernel from the per-frame cuboids (bit-identical)
         cub = coord_volumes
         _require_gpu(feat, proj, cub.params)
         V = cub.volume_size
         out = torch.empty((B, V, V, V, C), dtype=out_dtype, device=feat.device)
+        if out.numel() == 0:
+            return out
         code = _lib.load().mvn_unproject_cuboid(feat.data_ptr(), fd, proj.data_ptr(), cub.params.data_ptr(),
                                                 int(cub.transfer), None, out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC,
                                                 B, N, C, H, W, V, agg, int(align_corners), _stream(feat))
         _lib.check(code, "mvn_unproject_cuboid")
         return out
-    if isinstance(coord_volumes, Cuboids):
-        coord_volumes = coord_volumes.coord_volumes()
     coords = coord_volumes.float().contiguous()
     if coords.dim() != 5 or coords.shape[0] != B or coords.shape[4] != 3:
         raise RuntimeError(f"coord_volumes must be ({B}, Vx, Vy, Vz, 3), got {tuple(coords.shape)}")
     _require_gpu(feat, proj, coords)
     Vx, Vy, Vz = coords.shape[1:4]
     out = torch.empty((B, Vx, Vy, Vz, C), dtype=out_dtype, device=feat.device)
+    if out.numel() == 0:                  # empty batch: the empty volume, as unproject_heatmaps
+        return out
     code = _lib.load().mvn_unproject_ex(feat.data_ptr(), fd, proj.data_ptr(), coords.data_ptr(), None,
                                         out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC, B, N, C, H, W, Vx, Vy, Vz, agg,
                                         int(align_corners), _stream(feat))
@@ -134,6 +145,11 @@ def unproject_v2v_front(heatmaps, proj_matricies, coord_volumes, packed, scale, 
     B, N, C, H, W = feat.shape
     if C != CIN:
         raise RuntimeError(f"unproject_v2v_front needs {CIN} heatmap channels, got {C}")
+    if N > 8 or B == 0:
+        # more than 8 views (the channels-last kernels take N <= 8) or an empty batch: the two
+        # steps, which handle both
+        cl = unproject_channels_last(feat, proj, coord_volumes, volume_aggregation_method, align_corners=align_corners)
+        return v2v_front(cl, packed, scale, shift, out_dtype)
     if cub is not None:
         coords, V = None, cub.volume_size
         _require_gpu(feat, proj, cub.params, packed, scale, shift)

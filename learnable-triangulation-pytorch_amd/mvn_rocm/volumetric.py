@@ -70,6 +70,8 @@ class Cuboids:
         _require_gpu(self.params)
         B, V = self.batch, self.volume_size
         out = torch.empty((B, V, V, V, 3), dtype=torch.float32, device=self.device)
+        if out.numel() == 0:
+            return out
         # mvn_coord_volumes takes the four fields as separate (B, k) arrays
         fields = [self.params[:, 0:3].contiguous(), self.params[:, 3:6].contiguous(),
                   self.params[:, 6:9].contiguous(), self.params[:, 9:18].contiguous()]
@@ -96,7 +98,7 @@ def build_cuboids(base_points, cuboid_side: float, volume_size: int, theta=0.0, 
     position = (base - sides / 2).astype(np.float32)                               # :300, then f32 (:313)
     step = np.broadcast_to((sides / (V - 1)).astype(np.float32), (B, 3)).copy()     # :313-315
     centre = base.astype(np.float32)                                                 # :330
-    rot = np.stack([rotation_matrix(axis, t) for t in thetas]).astype(np.float32)    # volumetric.py:106
+    rot = (np.stack([rotation_matrix(axis, t) for t in thetas]) if B else np.zeros((0, 3, 3))).astype(np.float32)
     host = np.concatenate([position, centre, step, rot.reshape(B, 9)], axis=1)
     params = torch.from_numpy(np.ascontiguousarray(host)).to(torch.device(device))
     return Cuboids(params, V, transfer_cmu_to_human36m)

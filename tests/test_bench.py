@@ -29,3 +29,15 @@ def test_bench_spawns_the_ranks(gpus):
     assert line["config"]["global_batch"] == 8 * gpus and line["config"]["parallelism"] == f"dp{gpus}"
     assert line["gather_verified"] is True       # gathered joints == every frame built on rank 0
     assert line["steps"] == 3 and line["warmup"] == 1 and line["value"] > 0
+
+
+def test_bench_a_failing_rank_ends_the_job():
+    """Rank 1 dies before the first barrier (--dry-run-fail-rank): the launcher sees it while
+    rank 0 is still blocked in the barrier, terminates rank 0 and exits non-zero — instead of
+    waiting on rank 0 forever."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                           "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--dry-run-fail-rank", "1"], capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

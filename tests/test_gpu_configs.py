@@ -304,11 +304,52 @@ def test_empty_batch_matches_reference_behaviour(device):
     for method in ("sum", "softmax"):
         out = op.unproject_heatmaps(feat, P, coords, method)
         assert out.shape == (0, 8, 16, 16, 16) and out.dtype == torch.float32
+    # backward through the empty batch: the reference's autograd returns zero-sized gradients
+    feat_g = feat.clone().requires_grad_(True)
+    op.unproject_heatmaps(feat_g, P, coords, "softmax").sum().backward()
+    assert feat_g.grad is not None and feat_g.grad.shape == feat.shape
+    from mvn_rocm import volumetric
+    cub = volumetric.build_cuboids(np.zeros((0, 3)), 2500.0, 16, device=device)
+    feat_c = feat.clone().requires_grad_(True)
+    out = op.unproject_heatmaps(feat_c, P, cub, "sum")
+    assert out.shape == (0, 8, 16, 16, 16)
+    out.sum().backward()
+    assert feat_c.grad.shape == feat.shape
     ab = synth.algebraic_batch(1, 4, 17, seed=0)
     X = multiview.triangulate_batch_of_points(ab.proj[:0].to(device), ab.points[:0].to(device),
                                               ab.confidences[:0].to(device))
     assert X.shape == (0, 17, 3)
+    pts_g = ab.points[:0].to(device).requires_grad_(True)
+    conf_g = ab.confidences[:0].to(device).requires_grad_(True)
+    X = multiview.triangulate_batch_of_points(ab.proj[:0].to(device), pts_g, conf_g)
+    X.sum().backward()
+    assert pts_g.grad.shape == pts_g.shape and conf_g.grad.shape == conf_g.shape
     with pytest.raises(RuntimeError):
         op.integrate_tensor_3d_with_coordinates(torch.zeros((0, 17, 16, 16, 16), device=device), coords)
     with pytest.raises(RuntimeError):
         op.integrate_tensor_2d(torch.zeros((0, 17, 8, 8), device=device))
+
+
+@pytest.mark.gpu
+def test_channels_last_entry_points_empty_batch_and_many_views(device):
+    """The channels-last entry points handle what unproject_heatmaps handles: an empty batch
+    returns the empty volume without a launch, and more than 8 views (beyond the channels-last
+    kernels, mvn_hip.h) go through the NCDHW unprojection and a device permute — bit-identical
+    to it (sum) — and, for the one-call pipeline, through the two steps."""
+    from mvn_rocm import op, synth, v2v
+    vb = synth.volumetric_batch(1, n_views=10, channels=32, heatmap=24, volume=16, seed=5)
+    feat, P, coords = (t.to(device) for t in (vb.features, vb.proj, vb.coords))
+    cl = v2v.unproject_channels_last(feat, P, coords, "sum", out_dtype=torch.float32)
+    ref = op.unproject_heatmaps(feat, P, coords, "sum")
+    assert torch.equal(cl, ref.permute(0, 2, 3, 4, 1))
+    empty = v2v.unproject_channels_last(feat[:0], P[:0], coords[:0], "softmax")
+    assert empty.shape == (0, 16, 16, 16, 32) and empty.dtype == torch.bfloat16
+    g = torch.Generator().manual_seed(0)
+    packed, scale, shift = v2v.fold_basic3d_block(torch.randn((16, 32, 7, 7, 7), generator=g) * 0.02,
+                                                  torch.zeros(16), torch.ones(16), torch.zeros(16), torch.zeros(16),
+                                                  torch.ones(16), device=device)
+    y0 = v2v.unproject_v2v_front(feat[:0], P[:0], coords[:0], packed, scale, shift)
+    assert y0.shape == (0, 16, 16, 16, 16)
+    y = v2v.unproject_v2v_front(feat, P, coords, packed, scale, shift)
+    two = v2v.v2v_front(v2v.unproject_channels_last(feat, P, coords, "softmax"), packed, scale, shift)
+    assert torch.equal(y, two)

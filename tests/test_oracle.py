@@ -1,9 +1,11 @@
 """The oracle itself, pinned against vectors captured from the reference (CPU only)."""
+import os
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import max_rel
+from conftest import ROOT, max_rel
 from oracle import capi, restate_np, restate_torch
 
 METHODS = ("sum", "max", "softmax", "conf")
@@ -231,3 +233,50 @@ def test_chain_golden_pins_the_oracles(golden):
     x64 = restate_np.triangulate_batch_of_points(d["alg_proj"], kp2, conf)
     assert max_rel(x64, d["alg_kp3d64"]) <= 1e-6
     assert max_rel(d["alg_kp3d"], d["alg_kp3d64"]) <= 1e-3     # the f32 reference's own SVD error
+
+
+@pytest.mark.parametrize("method,ac,bf16", [("sum", 0, False), ("softmax", 1, False), ("conf", 0, False),
+                                            ("max", 0, True)])
+def test_oracle_under_address_sanitizer(golden, tmp_path, method, ac, bf16):
+    """SURVEY.md §5 (sanitizers): the C oracle built with -fsanitize=address,undefined
+    (oracle/asan_driver.c, every array in a malloc block of exactly its size) runs the golden
+    inputs — unprojection (out-of-image taps, behind-camera voxels, non-square maps), the
+    soft-argmax of its first channels and every DLT design matrix — with no sanitizer report,
+    and its outputs equal the regular build's (and, for sum, the reference golden) bit for bit."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"], check=True)
+    exe = os.path.join(ROOT, "oracle", "_build", "oracle_asan")
+    g = golden("unproject_small.npz")
+    feat = g["feat_bf16_bits"] if bf16 else g["feat"]
+    P, coords, conf = g["proj"], g["coords"], g["conf"]
+    B, N, C, H, W = feat.shape
+    Vx, Vy, Vz = coords.shape[1:4]
+    J = 3
+    rng = np.random.default_rng(7)
+    pts = rng.uniform(0, 20, (B, N, J, 2)).astype(np.float32)
+    pconf = rng.uniform(0.1, 1, (B, N, J)).astype(np.float32)
+    hdr = np.array([B, N, C, H, W, Vx, Vy, Vz, capi.agg_code(method), ac, int(bf16), J], np.int32)
+    blob = b"".join(np.ascontiguousarray(a).tobytes() for a in (hdr, feat, P, coords, conf, pts, pconf))
+    (tmp_path / "in.bin").write_bytes(blob)
+    r = subprocess.run([exe, str(tmp_path / "in.bin"), str(tmp_path / "out.bin")], capture_output=True, text=True,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-3000:]
+    out = np.frombuffer((tmp_path / "out.bin").read_bytes(), np.float32)
+    nv = Vx * Vy * Vz
+    vol = out[:B * C * nv].reshape(B, C, Vx, Vy, Vz)
+    ref = capi.unproject(feat, P, coords, method, conf, align_corners=bool(ac), feat_bf16_bits=bf16)
+    np.testing.assert_array_equal(vol, ref)
+    if method == "sum" and not bf16:
+        np.testing.assert_array_equal(vol, g[f"sum_ac{ac}"])
+    o = B * C * nv
+    xyz = out[o:o + B * J * 3].reshape(B, J, 3)
+    ref_xyz, ref_sv = capi.softargmax3d(np.ascontiguousarray(ref[:, :J]), coords, True, 1.0)
+    np.testing.assert_array_equal(xyz, ref_xyz)
+    o += B * J * 3
+    np.testing.assert_array_equal(out[o:o + B * J * nv].reshape(ref_sv.shape), ref_sv)
+    o += B * J * nv
+    A = out[o:].reshape(B, J, 2 * N, 4)
+    for b in range(B):
+        for j in range(J):
+            np.testing.assert_array_equal(A[b, j], capi.dlt_design(P, pts, pconf, b, j))

@@ -1,7 +1,9 @@
 """Scan gfx950 assembly for a VMEM store of more than 8 bytes (dwordx3 / dwordx4) whose
-data VGPRs are overwritten by the very next vector ALU instruction (no wait state between).
+data VGPRs a vector ALU instruction overwrites within the next WAIT_STATES (2) wait states.
 Such a store can read the NEW value (observed: channels-last unprojection, r14, channels 14-15
 nondeterministic), so every hit is a bug to fix in the source (a wait state / s_nop).
+Wait states after the store: every issued instruction counts one, `s_nop N` counts N + 1;
+an instruction is in the hazard window while fewer than WAIT_STATES have passed before it.
     python tools/check_store_hazard.py file.s|file.dis|lib.so [...]
 A shared library is unbundled (llvm-objdump --offloading, in a temporary directory) and its
 gfx950 code objects disassembled first; __graft_entry__.build() runs this on libmvn_hip.so."""
@@ -14,9 +16,11 @@ import sys
 import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
+WAIT_STATES = 2          # gfx940-class: a VALU write within 2 wait states of the store is a hazard
 
 STORE = re.compile(r"^\s*(buffer|global|flat)_store_dwordx([34])\s+(v\[(\d+):(\d+)\]|v(\d+)),?\s*(v\[(\d+):(\d+)\]|v\d+)?")
 DEST = re.compile(r"^\s*(v_[a-z0-9_]+)\s+v(?:\[(\d+):(\d+)\]|(\d+))")
+NOP = re.compile(r"^\s*s_nop\s+(0x[0-9a-fA-F]+|\d+)")
 
 
 def data_regs(m):
@@ -57,21 +61,24 @@ def scan(paths):
             if not m:
                 continue
             regs = data_regs(m)
-            j = i + 1
-            while j < len(lines) and (not lines[j].strip() or lines[j].strip().startswith(";")):
+            waited, j = 0, i + 1
+            while j < len(lines) and waited < WAIT_STATES:
+                ln2 = lines[j].strip()
                 j += 1
-            if j >= len(lines):
-                continue
-            d = DEST.match(lines[j])
-            if not d:
-                continue
-            if d.group(4) is not None:
-                w = {int(d.group(4))}
-            else:
-                w = set(range(int(d.group(2)), int(d.group(3)) + 1))
-            if w & regs:
-                hits += 1
-                print(f"{path}:{i + 1}: {fn[:90]}\n    {ln.strip()}\n    {lines[j].strip()}")
+                if not ln2 or ln2.startswith(";") or ln2.endswith(":"):
+                    continue                        # blank, comment, label
+                nop = NOP.match(ln2)
+                if nop:
+                    waited += int(nop.group(1), 0) + 1
+                    continue
+                d = DEST.match(ln2)
+                if d:
+                    w = {int(d.group(4))} if d.group(4) is not None else set(range(int(d.group(2)), int(d.group(3)) + 1))
+                    if w & regs:
+                        hits += 1
+                        print(f"{path}:{i + 1}: {fn[:90]}\n    {ln.strip()}\n    {ln2} (after {waited} wait state(s))")
+                        break
+                waited += 1
     return hits
 
 

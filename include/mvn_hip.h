@@ -301,6 +301,13 @@ int mvn_dlt_backward(const float* proj, const float* pts, const float* conf, con
  */
 int mvn_debug_set_unproject(int lds_slots, int kernel);
 
+/*
+ * Diagnostics: workgroups of the four-view unprojection kernel resident per CU (its LDS and
+ * register budget; the persistent grid is this x the CU count), for f32 (bf16_maps = 0) or
+ * bf16 (1) feature maps.  Needs a device; returns a count >= 1.
+ */
+int mvn_debug_unproject_occupancy(int bf16_maps);
+
 #ifdef __cplusplus
 }
 #endif

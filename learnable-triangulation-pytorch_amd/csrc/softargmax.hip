@@ -20,9 +20,6 @@
 // The finalize is the volume's last reader and its output is written once: both streams
 // non-temporal, so that they do not evict what the next launches read from the MALL (the
 // unprojection's feature maps and coordinates: bench step 292 -> 261 us at config 2).
-#ifndef MVN_SA_NT
-#define MVN_SA_NT 2      // A/B: 0 = plain, 1 = non-temporal stores only, 2 = stores and loads
-#endif
 
 namespace mvn {
 namespace {
@@ -34,21 +31,12 @@ constexpr int kSaBlock = 256;
 constexpr int kSaVpt = 16;                      // voxels per thread
 constexpr int kSaChunk = kSaBlock * kSaVpt;     // 4096 voxels per block
 constexpr int kPartial = 5;                     // m, s, sx, sy, sz
+constexpr bool kFinalNtLoads = true, kFinalNtStores = true;   // the finalize's streams (comment above)
 // voxels per pass-1 wave (all joints), per volume dtype; the workspace is sized for the
 // smaller.  1024 (16 voxels per lane in flight per joint, half the DPP reductions per voxel)
 // vs 512: config 2 soft-argmax 81.2 -> 76.2 us, config 3 186.1 -> 182.4 us (A/B, r09).
-#ifndef MVN_SA_PCHUNK_F32
-#define MVN_SA_PCHUNK_F32 1024
-#endif
-#ifndef MVN_SA_PCHUNK_BF16
-#define MVN_SA_PCHUNK_BF16 1024
-#endif
-template <typename T> constexpr int kPartChunkT = sizeof(T) == 4 ? MVN_SA_PCHUNK_F32 : MVN_SA_PCHUNK_BF16;
-constexpr int kPartChunkMin = MVN_SA_PCHUNK_F32 < MVN_SA_PCHUNK_BF16 ? MVN_SA_PCHUNK_F32 : MVN_SA_PCHUNK_BF16;
-
-#ifndef MVN_SA_MIN_WAVES
-#define MVN_SA_MIN_WAVES 0        // >0: split the joints of pass 1 over gridDim.z below this many waves (A/B r14: no gain)
-#endif
+template <typename T> constexpr int kPartChunkT = 1024;
+constexpr int kPartChunkMin = 1024;
 
 template <typename T> struct Vec;
 template <> struct Vec<float> { static constexpr int n = 4; };
@@ -434,7 +422,7 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_finalize(
   float t[RUNS][VEC];
 #pragma unroll
   for (int r = 0; r < RUNS; ++r)
-    load_run<T, VEC, (MVN_SA_NT >= 2)>(vj, chunk * kSaChunk + r * kSaBlock * VEC + tid * VEC, nvox, vec_ok, t[r], 0.f);
+    load_run<T, VEC, kFinalNtLoads>(vj, chunk * kSaChunk + r * kSaBlock * VEC + tid * VEC, nvox, vec_ok, t[r], 0.f);
 #pragma unroll
   for (int r = 0; r < RUNS; ++r) {
     const int i = chunk * kSaChunk + r * kSaBlock * VEC + tid * VEC;
@@ -445,13 +433,13 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_finalize(
       y[k] = SOFTMAX ? __expf(v - m) * inv : fmaxf(v, 0.f);
     }
     if constexpr (sizeof(TO) == sizeof(T)) {
-      store_run<TO, VEC, (MVN_SA_NT >= 1)>(oj, i, nvox, vec_ok, y);
+      store_run<TO, VEC, kFinalNtStores>(oj, i, nvox, vec_ok, y);
     } else {  // bf16 in -> f32 out: two float4 runs
       float lo[4] = {y[0], y[1], y[2], y[3]};
-      store_run<TO, 4, (MVN_SA_NT >= 1)>(oj, i, nvox, vec_ok, lo);
+      store_run<TO, 4, kFinalNtStores>(oj, i, nvox, vec_ok, lo);
       if constexpr (VEC == 8) {
         float hi[4] = {y[4], y[5], y[6], y[7]};
-        store_run<TO, 4, (MVN_SA_NT >= 1)>(oj, i + 4, nvox, vec_ok, hi);
+        store_run<TO, 4, kFinalNtStores>(oj, i + 4, nvox, vec_ok, hi);
       }
     }
   }
@@ -465,10 +453,9 @@ int launch(const void* vol, long long bs, long long js, const float* coords, con
   const bool vec_ok = (reinterpret_cast<uintptr_t>(vol) % 16 == 0) && (bs * sizeof(T)) % 16 == 0 &&
                       (js * sizeof(T)) % 16 == 0 && (nvox % 8 == 0) &&
                       (out == nullptr || reinterpret_cast<uintptr_t>(out) % 16 == 0);
-  // split the joints over gridDim.z when frames x chunks give fewer than MVN_SA_MIN_WAVES
-  // pass-1 waves (4 per SIMD); each joint's partial is computed the same way either way
-  const long long waves = (long long)B * npart;
-  const int nsplit = int(std::max(1LL, std::min<long long>(J, (MVN_SA_MIN_WAVES + waves - 1) / waves)));
+  // pass 1 takes every joint in one wave per chunk (gridDim.z = 1; splitting the joints over
+  // gridDim.z at small batches was measured and gave nothing, r14)
+  const int nsplit = 1;
   softargmax_partials<T, SOFTMAX><<<dim3((npart + kSaBlock / kWave - 1) / (kSaBlock / kWave), B, nsplit), kSaBlock, 0, st>>>(
       static_cast<const T*>(vol), bs, js, coords, cub, V, transfer, mult, part, J, nvox, npart, vec_ok);
   if (!launch_ok()) return MVN_ERR_LAUNCH;

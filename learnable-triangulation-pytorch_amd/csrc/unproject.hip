@@ -217,6 +217,16 @@ bool unproject_force_simple() { return g_force_simple.load(std::memory_order_rel
 bool unproject_force_generic() { return g_force_simple.load(std::memory_order_relaxed) == 2; }
 }  // namespace mvn
 
+namespace mvn {
+namespace unproj {
+int x4_blocks_per_cu(int bf16);
+}  // namespace unproj
+}  // namespace mvn
+
+extern "C" int mvn_debug_unproject_occupancy(int bf16_maps) {
+  return mvn::unproj::x4_blocks_per_cu(bf16_maps ? 1 : 0);
+}
+
 extern "C" int mvn_debug_set_unproject(int lds_slots, int kernel) {
   if (lds_slots < 0 || kernel < 0 || kernel > 2) return MVN_ERR_ARG;
   mvn::g_lds_slots.store(lds_slots, std::memory_order_relaxed);

@@ -317,19 +317,8 @@ __device__ __forceinline__ uint32_t chunk_px(const uint2& q, int p) {
   return (p & 1) ? (d & 0xffff0000u) : (d << 16);      // bf16 -> f32 bits, exact
 }
 
-// bf16 maps staged as bf16 (unproject_x4.hip, 8-byte slots): pixel p (0..3) of chunks ca, cb
-// as one word, channel a low (v_perm_b32 of the two halves)
-__device__ __forceinline__ uint32_t chunk_pair(const uint2& ca, const uint2& cb, int p) {
-  return __builtin_amdgcn_perm(p < 2 ? cb.x : cb.y, p < 2 ? ca.x : ca.y, (p & 1) ? 0x07060302u : 0x05040100u);
-}
-
 __device__ __forceinline__ f2 lo2(const uint4& q) { return f2{__uint_as_float(q.x), __uint_as_float(q.y)}; }
 __device__ __forceinline__ f2 hi2(const uint4& q) { return f2{__uint_as_float(q.z), __uint_as_float(q.w)}; }
-// channels (0, 1) / (2, 3) of an 8-byte slot of 4 bf16 channels, widened to f32 (exact)
-__device__ __forceinline__ f2 bf16_pair(uint32_t d) { return f2{__uint_as_float(d << 16), __uint_as_float(d & 0xffff0000u)}; }
-__device__ __forceinline__ f2 lo2(const uint2& q) { return bf16_pair(q.x); }
-__device__ __forceinline__ f2 hi2(const uint2& q) { return bf16_pair(q.y); }
-
 // View aggregation of a channel pair (op.py:147-161), lane-wise the op order of
 // aggregate<> (sum / max / conf, reference order; softmax, the unified formula).
 template <int AGG, int NV>
@@ -382,18 +371,14 @@ __device__ __forceinline__ f2 aggregate_pair(const f2 (&s)[NV], const f2 (&cf)[N
 // Cache policy of the four-view kernel's NCDHW output stores (2 = nt).  f32 planes stream
 // out non-temporally so that they do not evict the feature maps the next tiles re-read
 // (whole step at config 2: 261.5 -> 257.8 us); 2-byte bf16 stores must not (577 -> 1,664 us).
-#ifndef MVN_X4_STORE_POLICY
-#define MVN_X4_STORE_POLICY 0
-#endif
-#ifndef MVN_X4_STORE_POLICY_F32
-#define MVN_X4_STORE_POLICY_F32 2
-#endif
+constexpr int kStorePolicyF32 = 2;     // nt
+constexpr int kStorePolicyBf16 = 0;    // default
 template <typename T> __device__ __forceinline__ void store_plane(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
 template <> __device__ __forceinline__ void store_plane<float>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, MVN_X4_STORE_POLICY_F32);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, kStorePolicyF32);
 }
 template <> __device__ __forceinline__ void store_plane<uint16_t>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
-  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, MVN_X4_STORE_POLICY);
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, kStorePolicyBf16);
 }
 
 // Per-view region of the LDS image (block-uniform, SGPRs).

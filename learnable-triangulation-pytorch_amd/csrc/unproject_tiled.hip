@@ -37,9 +37,6 @@ namespace {
 
 // 4 views: skip, per wave, staged slots past the tile's footprint (A/B r04: 194.2 -> 191.1 us
 // at config 2, bit-identical); 8 views stage every slot a thread owns (1,031 vs 1,061 us).
-#ifndef MVN_STAGE_UNCOND
-#define MVN_STAGE_UNCOND 0   // 1: stage every slot unconditionally for 4 views as well
-#endif
 
 
 // Tile of voxels per block (z fastest: a wave's output stores are 16-voxel = 64-byte runs
@@ -55,12 +52,8 @@ template <> struct TileShape<4> { static constexpr int TX = 4, TY = 8, TZ = 16, 
 // blocks share a CU (one block's prologue / barriers overlap the other's staging and
 // sampling): config 4 1,278 -> 1,027 us at 16 frames, bit-identical (A/B).
 // The 4-view kernel keeps 16-byte slots (2-channel slots at 6 waves/SIMD: no gain).
-#ifndef MVN_G_8VIEWS
-#define MVN_G_8VIEWS 2
-#endif
 template <> struct TileShape<8> {
-  static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 4096, G = MVN_G_8VIEWS;
-  static constexpr int WAVES = G == 2 ? 4 : 2;
+  static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 4096, G = 2, WAVES = 4;
 };
 
 template <typename T> __device__ __forceinline__ uint32_t buf_load(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
@@ -72,14 +65,11 @@ template <> __device__ __forceinline__ uint32_t buf_load<uint16_t>(__amdgpu_buff
 }
 
 template <typename T> __device__ __forceinline__ void buf_store(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
-#ifndef MVN_TILED_STORE_POLICY_F32
-#define MVN_TILED_STORE_POLICY_F32 2   // f32 planes non-temporal (A/B: 8 views, step 1,195 -> 1,179 us at 16 frames)
-#endif
-#ifndef MVN_TILED_XCD_MIN_FRAMES
-#define MVN_TILED_XCD_MIN_FRAMES 16
-#endif
+// f32 planes non-temporal (A/B: 8 views, step 1,195 -> 1,179 us at 16 frames); XCD slabs from
+// 16 frames on
+constexpr int kTiledStorePolicyF32 = 2, kTiledXcdMinFrames = 16;
 template <> __device__ __forceinline__ void buf_store<float>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, MVN_TILED_STORE_POLICY_F32);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, kTiledStorePolicyF32);
 }
 template <> __device__ __forceinline__ void buf_store<uint16_t>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
   __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, 0);
@@ -185,7 +175,7 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
   int L = int(blockIdx.x);
   {
     const int nf = nTx * nTy * nTz;
-    if (B >= MVN_TILED_XCD_MIN_FRAMES && nf % 8 == 0) {
+    if (B >= kTiledXcdMinFrames && nf % 8 == 0) {
       const int xcd = int(blockIdx.x) % 8, k = int(blockIdx.x) / 8, slab = nf / 8;
       L = (k / slab) * nf + xcd * slab + k % slab;
     }
@@ -404,7 +394,7 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
       goff[i] = in ? uint32_t((q.v * C * HW + gy * W + gx) * int(sizeof(TIn))) : kOob;
     }
     uint32_t pre[MS][G];
-    constexpr bool UNCOND = NV == 8 || MVN_STAGE_UNCOND;
+    constexpr bool UNCOND = NV == 8;
     auto issue = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < MS; ++i)

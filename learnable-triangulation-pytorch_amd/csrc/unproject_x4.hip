@@ -24,74 +24,7 @@
 // in flight, XCD-balanced block order, buffer-descriptor stores — follows unproject_tiled.
 // Footprints that exceed one LDS buffer are staged in several passes of whole views;
 // a single view larger than a buffer sends its block to the global-gather fallback.
-#include <type_traits>
-
 #include "unproject_common.hpp"
-
-// Ablation switches for A/B builds (tools/build_x4_variant.sh); all 0 in the library.
-#ifndef MVN_X4_ABL_NOSTORE
-#define MVN_X4_ABL_NOSTORE 0   // 1: outputs stored only if the value equals a sentinel (no traffic)
-#endif
-#ifndef MVN_X4_ABL_NOSTAGE
-#define MVN_X4_ABL_NOSTAGE 0   // 1: stage the first channel group only (later groups reuse it)
-#endif
-#ifndef MVN_X4_ABL_BCAST
-#define MVN_X4_ABL_BCAST 0     // 1: every lane reads its wave's first lane's taps (no bank conflicts)
-#endif
-
-#ifndef MVN_X4_STAMPS
-#define MVN_X4_STAMPS 0        // 1: diagnostic build, per-block phase timestamps (mvn_x4_stamps)
-#endif
-#if MVN_X4_STAMPS
-__device__ unsigned long long g_x4_stamps[1 << 21];
-#define X4_STAMP(i)                                                                            \
-  do {                                                                                         \
-    if (threadIdx.x == 0 && blockIdx.x < (1u << 21) / 16)                                      \
-      g_x4_stamps[blockIdx.x * 16 + (i)] = (i) == 0 ? __builtin_amdgcn_s_memrealtime()         \
-                                                    : __builtin_amdgcn_s_memtime();            \
-  } while (0)
-#define X4_ACC_DECL unsigned long long x4_acc[4] = {0, 0, 0, 0}, x4_t = __builtin_amdgcn_s_memtime()
-#define X4_ACC(k)                                                                              \
-  do {                                                                                         \
-    const unsigned long long x4_n = __builtin_amdgcn_s_memtime();                              \
-    x4_acc[k] += x4_n - x4_t;                                                                  \
-    x4_t = x4_n;                                                                               \
-  } while (0)
-#define X4_ACC_STORE                                                                           \
-  do {                                                                                         \
-    if (threadIdx.x == 0 && blockIdx.x < (1u << 21) / 16)                                      \
-      for (int k = 0; k < 4; ++k) g_x4_stamps[blockIdx.x * 16 + 8 + k] = x4_acc[k];           \
-  } while (0)
-#else
-#define X4_STAMP(i) do {} while (0)
-#define X4_ACC_DECL do {} while (0)
-#define X4_ACC(k) do {} while (0)
-#define X4_ACC_STORE do {} while (0)
-#endif
-
-#ifndef MVN_X4_TILE
-#define MVN_X4_TILE -1   // voxel tile: 0 = 4x8x16 (512 threads), 1 = 8x8x8 (512), 2 = 4x8x8 (256), -1 = per dtype
-#endif
-#ifndef MVN_X4_XCD_MIN_FRAMES
-#define MVN_X4_XCD_MIN_FRAMES 1    // from this many frames each XCD takes the same slab of every frame
-#endif
-#ifndef MVN_X4_LDS_STORE
-#define MVN_X4_LDS_STORE 0          // 1: bf16 NCDHW output rows of TZ voxels gathered in LDS, 16-byte
-#endif                              //    stores (r10: 583 -> 567 us at config 3; since the stores are
-                                    //    deferred past the next commit the direct 2-byte stores win:
-                                    //    542 -> 530 us, profiles/r14_ab.txt)
-#ifndef MVN_X4_LDS_STORE_POLICY
-#define MVN_X4_LDS_STORE_POLICY 0   // cache policy of those 16-byte stores (2 = nt)
-#endif
-#ifndef MVN_X4_PATCH_LANES
-#define MVN_X4_PATCH_LANES 1        // lane groups of ds_read_b128 take compact 2 x 8 (y, z) voxel patches
-#endif
-#ifndef MVN_X4_BF16_LDS
-#define MVN_X4_BF16_LDS 0           // 1: bf16 maps staged as bf16, 8-byte LDS slots of 4 channels
-#endif                              //    (bit-identical; cfg3 533 -> 570 us: the widening VALU costs more)
-#ifndef MVN_X4_CL_GROUPS
-#define MVN_X4_CL_GROUPS 4          // bf16 channels-last: channel groups per run of 16-byte stores (1, 2, 4)
-#endif
 
 namespace mvn {
 namespace unproj {
@@ -102,24 +35,12 @@ namespace {
 // the largest footprints 2,156 / 1,428 / 965 slots (tools: /tmp-free model in DESIGN.md).
 template <int K> struct X4Shape;
 template <> struct X4Shape<0> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, MC = 2, WAVES = 4; };
-template <> struct X4Shape<1> { static constexpr int TX = 8, TY = 8, TZ = 8, THREADS = 512, SLOTS = 1536, MC = 2, WAVES = 4; };
-#ifndef MVN_X4_T2_SLOTS
-#define MVN_X4_T2_SLOTS 1024
-#endif
-#ifndef MVN_X4_T2_WAVES
-#define MVN_X4_T2_WAVES 4
-#endif
-template <> struct X4Shape<2> {
-  static constexpr int TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = MVN_X4_T2_SLOTS, MC = 2, WAVES = MVN_X4_T2_WAVES;
-};
+template <> struct X4Shape<2> { static constexpr int TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 1024, MC = 2, WAVES = 4; };
 
-#ifndef MVN_X4_PACKED_REGIONS
-#define MVN_X4_PACKED_REGIONS 1
-#endif
-// Per-view LDS regions (block-uniform, scalar registers).  Unpacked: 12 SGPRs per view (48
-// for 4 views, which spilled to VGPR lanes: ~60 v_writelane / v_readlane in the prologue);
-// packed: 3 words per view — (x0 + 1, y0 + 1), (bw, bh), sbase | cbase << 13 | pass << 24 —
-// and the derived fields recomputed on use.
+// Per-view LDS regions (block-uniform, scalar registers), packed 3 words per view —
+// (x0 + 1, y0 + 1), (bw, bh), sbase | cbase << 13 | pass << 24 — the derived fields
+// recomputed on use (unpacked, the 48 SGPRs of 4 views spilled to VGPR lanes: ~60
+// v_writelane / v_readlane in the prologue, round 2).
 __device__ __forceinline__ Region make_region(int x0, int y0, int bw, int bh, int sbase, int cbase, int pass) {
   Region r;
   r.x0 = x0; r.y0 = y0; r.bw = bw; r.bh = bh; r.sbase = sbase; r.cbase = cbase; r.pass = pass;
@@ -132,13 +53,7 @@ __device__ __forceinline__ Region make_region(int x0, int y0, int bw, int bh, in
   r.inv_cw = r.cw ? __builtin_amdgcn_rcpf(float(r.cw)) : 0.f;
   return r;
 }
-template <bool PACKED> struct RegionSet {
-  Region rg[4];
-  __device__ __forceinline__ void set(int v, const Region& r) { rg[v] = r; }
-  __device__ __forceinline__ Region get(int v) const { return rg[v]; }
-  __device__ __forceinline__ Region pick(int u) const { return pick_region(rg, u); }
-};
-template <> struct RegionSet<true> {
+struct RegionSet {
   uint32_t a[4], b[4], c[4];
   __device__ __forceinline__ void set(int v, const Region& r) {
     a[v] = uint32_t(r.x0 + 1) | (uint32_t(r.y0 + 1) << 16);
@@ -178,28 +93,21 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   // per buffer: image slots [0, kTrash), 64 per-lane trash slots (the masked-off pixels of
   // a chunk are written there: no exec-mask branch per write), 2 zero slots
   constexpr int kZeroSlot = kBuf - 2, kTrash = kBuf - 2 - kWave;
-  // LDS slot = one pixel's G channels: f32 (16 bytes), or bf16 maps kept as bf16 (8 bytes:
-  // half the LDS bytes written and read per channel; a tap's pairs are widened to f32 on the
-  // read side, exactly)
-  constexpr bool kB16 = MVN_X4_BF16_LDS && sizeof(TIn) == 2;
-  using Slot = typename std::conditional<kB16, uint2, uint4>::type;
+  // LDS slot = one pixel's G channels as f32 (16 bytes; bf16 maps are widened exactly when
+  // staged: bf16 slots halve the LDS bytes but the per-tap widening costs more VALU, r13)
+  using Slot = uint4;
   constexpr uint32_t kSlotB = sizeof(Slot);
   constexpr uint32_t E = sizeof(TIn);
 
   __shared__ Slot stage[2 * kBuf];
   __shared__ int red[kWaves][NV][4];
-  // bf16 NCDHW output: each group's G channel planes of the tile gathered in LDS (double
-  // buffered), then stored as 16-byte rows (TZ = 8 voxels) one barrier later — instead of
-  // one 2-byte store per voxel and channel
-  constexpr bool kLdsOut = MVN_X4_LDS_STORE && sizeof(TOut) == 2 && TZ * sizeof(TOut) == 16;
-  __shared__ uint16_t ost[kLdsOut ? 2 * G * kThreads : 1];
 
   // ---- which tile (z-tiles fastest; block order as unproject_tiled) ------------------
   const int nTx = (Vx + TX - 1) / TX, nTy = (Vy + TY - 1) / TY, nTz = (Vz + TZ - 1) / TZ;
   int L = int(blockIdx.x);
   {
     const int nf = nTx * nTy * nTz;
-    if (B >= MVN_X4_XCD_MIN_FRAMES && nf % 8 == 0) {
+    if (nf % 8 == 0) {
       const int xcd = int(blockIdx.x) % 8, k = int(blockIdx.x) / 8, slab = nf / 8;
       L = (k / slab) * nf + xcd * slab + k % slab;
     }
@@ -212,8 +120,6 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int nvox = Vx * Vy * Vz;
   const int HW = H * W;
-  X4_STAMP(0);
-  X4_STAMP(1);
   const float* Pb = P + size_t(b) * NV * 12;
   const TIn* fb = feat + size_t(b) * NV * C * HW;
   const float* cfb = conf ? conf + size_t(b) * NV * C : nullptr;
@@ -229,8 +135,8 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   // taps land on fewer, closer pixels: fewer LDS bank conflicts (tools/lds_conflicts.py
   // model: 9.3 -> 7.6 cycles per read at 4x8x16, 9.1 -> 7.9 at 4x8x8) than z-fastest lanes.
   // vt = the voxel's index in the tile (x, y, z row-major).
-  int vt = t;
-  if (MVN_X4_PATCH_LANES) {
+  int vt;
+  {
     const int m = lane & 31;
     const bool g1 = (m >= 4 && m < 12) || (m >= 16 && m < 20) || m >= 28;
     const int i = g1 ? (m < 12 ? m - 4 : m < 20 ? m - 8 : m - 16) : (m < 4 ? m : m < 16 ? m - 8 : m - 12);
@@ -239,7 +145,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     const int yw = 2 * (g / ZH) + (i >> 3), z = 8 * (g % ZH) + (i & 7);
     vt = (t & ~(kWave - 1)) + yw * TZ + z;
   }
-  static_assert(!MVN_X4_PATCH_LANES || (TZ % 8 == 0 && kWave % TZ == 0 && (kWave / TZ) * (TZ / 8) == 8),
+  static_assert(TZ % 8 == 0 && kWave % TZ == 0 && (kWave / TZ) * (TZ / 8) == 8,
                 "patch lanes: a wave is 2 x 8-voxel rows per lane group");
   const int X = X0 + vt / (TZ * TY), Y = Y0 + (vt / TZ) % TY, Z = Z0 + vt % TZ;
   const bool act = (X < Vx) & (Y < Vy) & (Z < Vz);
@@ -282,7 +188,6 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
 
   // ---- per-view boxes (ints, clipped to the pixels a tap can start at) ----------------
   int box[NV][4];
-  X4_STAMP(2);
   {
     // exact: every voxel's base pixel.  The 16 per-wave reductions (4 views x min x0, max x1,
     // min y0, max y1; maxima as minima of negated values) run as one transposing butterfly:
@@ -338,10 +243,9 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
         box[v][k] = (k & 1) ? -m : m;
       }
   }
-  X4_STAMP(3);
 
   // ---- LDS regions (slots and chunks), in scalar registers ----------------------------
-  RegionSet<MVN_X4_PACKED_REGIONS != 0> rs;
+  RegionSet rs;
   int npass, total;
   {
     int snext = 0, cnext = 0, pass = 0, chunks0 = 0;
@@ -366,7 +270,6 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     npass = too_big ? -1 : pass + 1;
     total = chunks0;
   }
-  X4_STAMP(4);
 
   if (npass < 0) {
     // A single view's footprint exceeds the LDS buffer: gather straight from global memory.
@@ -379,7 +282,6 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   const __amdgpu_buffer_rsrc_t frs = make_rsrc(fb, uint32_t(size_t(NV) * C * HW * E));
   const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + size_t(b) * C * nvox, uint32_t(size_t(C) * nvox * sizeof(TOut)));
   const uint32_t ooff = act ? uint32_t(vox) * uint32_t(sizeof(TOut)) : kOob;
-  const bool lds_out = kLdsOut && !out_cl && (X0 + TX <= Vx) && (Y0 + TY <= Vy) && (Z0 + TZ <= Vz);
   const uint32_t ooff_cl = act ? uint32_t(vox) * uint32_t(C) * uint32_t(sizeof(TOut)) : kOob;
 
   // LDS byte offsets of each view's north-west and south-west taps (the exact boxes contain
@@ -394,10 +296,6 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       const int slot = rv.sbase + dy * rv.pitch + dx;
       anw[v] = uint32_t(use ? slot : kZeroSlot) * kSlotB;
       asw[v] = uint32_t(use ? slot + rv.pitch : kZeroSlot) * kSlotB;
-      if (MVN_X4_ABL_BCAST) {
-        anw[v] = __builtin_amdgcn_readfirstlane(anw[v]);
-        asw[v] = __builtin_amdgcn_readfirstlane(asw[v]);
-      }
     }
   };
   // Chunk (k of a pass) -> global byte offset (kOob outside the image), first LDS slot and
@@ -427,11 +325,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   auto write_group = [&](Slot* buf, const Chunk (&pre)[G], int s0, uint32_t mask) __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      Slot q;
-      if constexpr (kB16)
-        q = make_uint2(chunk_pair(pre[0], pre[1], p), chunk_pair(pre[2], pre[3], p));
-      else
-        q = make_uint4(chunk_px(pre[0], p), chunk_px(pre[1], p), chunk_px(pre[2], p), chunk_px(pre[3], p));
+      const Slot q = make_uint4(chunk_px(pre[0], p), chunk_px(pre[1], p), chunk_px(pre[2], p), chunk_px(pre[3], p));
       if constexpr (sizeof(TIn) == 2)
         buf[(mask & (1u << p)) ? s0 + p : kTrash + lane] = q;
       else if (mask & (1u << p))
@@ -454,9 +348,10 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight
     }
   };
-  uint2 cl_buf[MVN_X4_CL_GROUPS > 1 ? MVN_X4_CL_GROUPS - 1 : 1];
+  constexpr int NG = 4;                    // bf16 channels-last: groups per run of 16-byte stores
+  uint2 cl_buf[NG - 1];
 #pragma unroll
-  for (int k = 0; k < (MVN_X4_CL_GROUPS > 1 ? MVN_X4_CL_GROUPS - 1 : 1); ++k) cl_buf[k] = make_uint2(0u, 0u);
+  for (int k = 0; k < NG - 1; ++k) cl_buf[k] = make_uint2(0u, 0u);
   auto aggregate = [&](int c0, const f2 (&sv)[2][NV], float (&r)[G]) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -470,16 +365,16 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       r[2 * q + 1] = o.y;
     }
   };
-  // The group's G output values of this voxel: to global memory, or (bf16 NCDHW tiles) to
-  // the LDS row buffer that flush() stores after the next barrier.
-  auto store_out = [&](int c0, const float (&r)[G], bool to_lds) __attribute__((always_inline)) {
+  // The group's G output values of this voxel: NCDHW planes, or the voxel's channels-last
+  // record (config 5).  bf16 NCDHW planes are direct 2-byte stores (r14: once the stores were
+  // deferred past the next commit they beat 16-byte rows gathered through LDS, 542 -> 530 us).
+  auto store_out = [&](int c0, const float (&r)[G]) __attribute__((always_inline)) {
     if (out_cl) {
       // c0 is block-uniform; readfirstlane keeps it scalar (soffset operands must be SGPRs)
       const uint32_t soff = __builtin_amdgcn_readfirstlane(uint32_t(c0) * uint32_t(sizeof(TOut)));
-      if constexpr (sizeof(TOut) == 2 && MVN_X4_CL_GROUPS > 1) {
-        // bf16 channels-last: MVN_X4_CL_GROUPS groups' 8-byte pieces of the voxel's record are
-        // held in registers and go out as 16-byte stores of consecutive channels
-        constexpr int NG = MVN_X4_CL_GROUPS;
+      if constexpr (sizeof(TOut) == 2) {
+        // bf16 channels-last: NG groups' 8-byte pieces of the voxel's record are held in
+        // registers and go out as 16-byte stores of consecutive channels
         const uint2 cur = make_uint2(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[2], r[3]));
         const int gi = (c0 / G) % NG;
         if (gi == NG - 1) {
@@ -507,48 +402,17 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
         }
         return;
       }
-      if constexpr (sizeof(TOut) == 4)
-        store_b128_padded(
-            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
-                               make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]),
-                                          __float_as_uint(r[3]))),
-            ors, ooff_cl, soff);
-      else
-        __builtin_amdgcn_raw_buffer_store_b64(
-            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int,
-                               make_uint2(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[2], r[3]))),
-            ors, ooff_cl, soff, 0);
-      return;
-    }
-    if (kLdsOut && to_lds) {
-      uint16_t* o = ost + ((c0 / G) & 1) * (G * kThreads) + vt;
-#pragma unroll
-      for (int ch = 0; ch < G; ++ch) o[ch * kThreads] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r[ch]));
+      store_b128_padded(
+          __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
+                             make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]),
+                                        __float_as_uint(r[3]))),
+          ors, ooff_cl, soff);
       return;
     }
 #pragma unroll
     for (int ch = 0; ch < G; ++ch)
-      if (!MVN_X4_ABL_NOSTORE || r[ch] == 1234.5f)
-        store_plane<TOut>(r[ch], ors, ooff, uint32_t(c0 + ch) * uint32_t(nvox) * uint32_t(sizeof(TOut)));
+      store_plane<TOut>(r[ch], ors, ooff, uint32_t(c0 + ch) * uint32_t(nvox) * uint32_t(sizeof(TOut)));
   };
-  // the 16-byte rows of group c0 (after the barrier that follows its consume)
-  auto flush = [&](int c0) __attribute__((always_inline)) {
-    if constexpr (kLdsOut) {
-      constexpr int kRows = G * TX * TY;                      // one row = TZ voxels of one channel
-      if (!lds_out || t >= kRows) return;
-      const int ch = t / (TX * TY), row = t - ch * (TX * TY);
-      const uint4 q = *reinterpret_cast<const uint4*>(ost + ((c0 / G) & 1) * (G * kThreads) + ch * kThreads + row * TZ);
-      const int x = row / TY, y = row - x * TY;
-      // the lane's channel plane goes in the VGPR offset, the group's first plane in the
-      // scalar one (a per-lane soffset compiles into a readfirstlane waterfall loop)
-      const uint32_t voff = uint32_t(((X0 + x) * Vy + (Y0 + y)) * Vz + Z0) * uint32_t(sizeof(TOut)) +
-                            uint32_t(ch) * uint32_t(nvox) * uint32_t(sizeof(TOut));
-      const uint32_t soff = __builtin_amdgcn_readfirstlane(uint32_t(c0) * uint32_t(nvox) * uint32_t(sizeof(TOut)));
-      store_b128_padded<MVN_X4_LDS_STORE_POLICY>(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, q),
-                                                 ors, voff, soff);
-    }
-  };
-
   auto consume = [&](const Slot* buf, int c0, float (&r)[G]) __attribute__((always_inline)) {
     f2 sv[2][NV];
     sample_views(reinterpret_cast<const char*>(buf), true, 0, sv);
@@ -571,67 +435,43 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       const Region r = rs.pick(sel);
       chunk_fields(r, sel, k - r.cbase, goff[i], s0[i], mask[i], k < total);
     }
-    X4_STAMP(12);
     const int wfirst = __builtin_amdgcn_readfirstlane(wid * kWave);
     Chunk pre[MC][G];
     auto issue = [&](int c0) __attribute__((always_inline)) {
-      if (MVN_X4_ABL_NOSTAGE && c0 >= 2 * G) return;
 #pragma unroll
       for (int i = 0; i < MC; ++i)
         if (wfirst + kThreads * i < total) load_group(pre[i], goff[i], c0);
     };
-    int ncommit = 0;
     auto commit = [&](Slot* buf) __attribute__((always_inline)) {
-      if (MVN_X4_ABL_NOSTAGE && ncommit++ >= 2) return;
 #pragma unroll
       for (int i = 0; i < MC; ++i)
         if (wfirst + kThreads * i < total) write_group(buf, pre[i], s0[i], mask[i]);
     };
     issue(0);
-    X4_STAMP(5);
     tap_slots();
     commit(stage);
     __syncthreads();
-    X4_STAMP(6);
-    X4_ACC_DECL;
     // A group's outputs are stored after the NEXT group's commit: on gfx950 vmcnt counts
     // stores as well as loads, in issue order, so stores issued at the end of a consume made
     // the commit's wait for the next group's loads also wait for their write acknowledgement.
-    int last = 0;
     float r[G];
     for (int c0 = 0; c0 < C; c0 += 2 * G) {
       const bool more1 = c0 + G < C, more2 = c0 + 2 * G < C;
       if (more1) issue(c0 + G);
-      X4_ACC(3);
       consume(stage, c0, r);
-      X4_ACC(0);
-      if (!more1) { store_out(c0, r, lds_out); last = c0; break; }
+      if (!more1) { store_out(c0, r); break; }
       commit(stage + kBuf);
       __builtin_amdgcn_sched_barrier(0);
-      store_out(c0, r, lds_out);
-      X4_ACC(1);
+      store_out(c0, r);
       __syncthreads();
-      flush(c0);
-      X4_ACC(2);
       if (more2) issue(c0 + 2 * G);
-      X4_ACC(3);
       consume(stage + kBuf, c0 + G, r);
-      X4_ACC(0);
-      if (!more2) { store_out(c0 + G, r, lds_out); last = c0 + G; break; }
+      if (!more2) { store_out(c0 + G, r); break; }
       commit(stage);
       __builtin_amdgcn_sched_barrier(0);
-      store_out(c0 + G, r, lds_out);
-      X4_ACC(1);
+      store_out(c0 + G, r);
       __syncthreads();
-      flush(c0 + G);
-      X4_ACC(2);
     }
-    if (kLdsOut && lds_out) {                 // the last group's rows
-      __syncthreads();
-      flush(last);
-    }
-    X4_STAMP(7);
-    X4_ACC_STORE;
     return;
   }
 
@@ -660,17 +500,11 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     }
     float r[G];
     aggregate(c0, sv, r);
-    store_out(c0, r, false);
+    store_out(c0, r);
   }
 }
 
 }  // namespace
-
-#if MVN_X4_STAMPS
-extern "C" int mvn_x4_stamps(void* dst, size_t bytes) {
-  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_x4_stamps), bytes) == hipSuccess ? 0 : -1;
-}
-#endif
 
 // Returns MVN_OK, an error code, or 1 when this kernel does not apply (the caller then
 // runs unproject_tiled).
@@ -685,7 +519,7 @@ int launch_x4(const void* feat, const float* P, const float* coords, const float
   const int knob = unproject_lds_slot_budget();
   const int budget = knob > 0 ? knob : 1 << 30;
   // tile per input dtype (A/B at the bench configs): f32 4x8x16, bf16 4x8x8
-  constexpr int K = MVN_X4_TILE >= 0 ? MVN_X4_TILE : (sizeof(TIn) == 2 ? 2 : 0);
+  constexpr int K = sizeof(TIn) == 2 ? 2 : 0;
   using S = X4Shape<K>;
   const long long nb = (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) *
                        ((Vz + S::TZ - 1) / S::TZ);
@@ -694,6 +528,17 @@ int launch_x4(const void* feat, const float* P, const float* coords, const float
       static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, C, H, W, Vx, Vy,
       Vz, align_corners, budget, out_cl);
   return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
+}
+
+// Diagnostics (mvn_debug_unproject_occupancy): resident blocks per CU of the softmax kernels.
+int x4_blocks_per_cu(int bf16) {
+  int n = 0;
+  const hipError_t e =
+      bf16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, unproject_x4<MVN_AGG_SOFTMAX, uint16_t, uint16_t, 2>,
+                                                          X4Shape<2>::THREADS, 0)
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, unproject_x4<MVN_AGG_SOFTMAX, float, float, 0>,
+                                                          X4Shape<0>::THREADS, 0);
+  return e == hipSuccess ? n : MVN_ERR_LAUNCH;
 }
 
 #define MVN_INSTANTIATE(AGG)                                                                                   \

@@ -61,6 +61,7 @@ SIGNATURES = {
                                   + [_c_int] * 5 + [_c_void_p]),
     "mvn_dlt_backward": (_c_int, [_c_void_p] * 6 + [_c_int, _c_int, _c_int, _c_void_p]),
     "mvn_debug_set_unproject": (_c_int, [_c_int, _c_int]),
+    "mvn_debug_unproject_occupancy": (_c_int, [_c_int]),
 }
 
 _lib = None

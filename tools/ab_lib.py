@@ -23,6 +23,10 @@ def load(path):
 
 def main():
     libs = [(os.path.basename(p), load(p)) for p in sys.argv[1:]]
+    for name, lib in libs:
+        if hasattr(lib, "mvn_debug_unproject_occupancy"):
+            print(f"{name}: x4 blocks per CU f32 {lib.mvn_debug_unproject_occupancy(0)} "
+                  f"bf16 {lib.mvn_debug_unproject_occupancy(1)}", flush=True)
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
     cases = [(8, 4, torch.float32, "cfg2 f32 B=8"), (32, 4, torch.bfloat16, "cfg3 bf16 B=32")]

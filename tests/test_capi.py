@@ -132,3 +132,22 @@ def test_unproject_v2v_front_argument_validation(lib):
     assert call(V=40) == -2
     assert call(ws=None) == -5
     assert call(wsb=ws - 1) == -5
+
+
+def test_deterministic_backward_argument_checks(lib):
+    """mvn_unproject_backward_deterministic validates before any HIP call: the workspace
+    (64-bit fixed-point sums: one per feature element and per confidence) must be present and
+    large enough (MVN_ERR_WORKSPACE), shapes and enums as mvn_unproject_backward."""
+    B, N, C, H, W = 2, 4, 8, 24, 24
+    need = lib.mvn_unproject_backward_workspace_bytes(B, N, C, H, W)
+    assert need == (B * N * C * H * W + B * N * C) * 8
+    assert lib.mvn_unproject_backward_workspace_bytes(0, N, C, H, W) == 0
+
+    def call(ws=1, ws_bytes=need, agg=0, B_=B, N_=N):
+        return lib.mvn_unproject_backward_deterministic(1, 0, 1, 1, None, 1, 0, 1, None, ws, ws_bytes, B_, N_, C, H,
+                                                        W, 16, 16, 16, agg, 0, None)
+    assert call(ws=None) == -5
+    assert call(ws_bytes=need - 1) == -5
+    assert call(agg=7) == -1
+    assert call(B_=0) == -2
+    assert call(N_=9) == -2

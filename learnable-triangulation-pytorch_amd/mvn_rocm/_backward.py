@@ -13,10 +13,10 @@ import torch
 from torch import Tensor
 
 from . import _lib
-from ._ops import _DTYPE_CODE, _ptr, _require_gpu, _stream
+from ._ops import _DTYPE_CODE, _op, _ptr, _require_gpu, _stream, call
 
 
-@torch.library.custom_op("mvn_rocm::unproject_backward", mutates_args=())
+@_op("unproject_backward")
 def unproject_bwd(feat: Tensor, proj: Tensor, coords: Tensor, conf: Optional[Tensor], grad_out: Tensor, agg: int,
                   align_corners: bool, want_conf: bool) -> List[Tensor]:
     """-> [grad_feat (B,N,C,H,W) in feat's dtype, grad_conf (B,N,C) f32 (empty unless want_conf)]"""
@@ -58,7 +58,7 @@ def _(feat, proj, coords, conf, grad_out, agg, align_corners, want_conf):
     return [torch.empty_like(feat), feat.new_empty((B, N, C) if want_conf else (0,), dtype=torch.float32)]
 
 
-@torch.library.custom_op("mvn_rocm::softargmax3d_backward", mutates_args=())
+@_op("softargmax3d_backward")
 def softargmax3d_bwd(vol: Tensor, coords: Tensor, softmax: bool, multiplier: float, grad_xyz: Optional[Tensor],
                      grad_vol: Optional[Tensor]) -> Tensor:
     """-> grad w.r.t. vol (B,J,Vx,Vy,Vz), contiguous, vol's dtype."""
@@ -85,7 +85,7 @@ def _(vol, coords, softmax, multiplier, grad_xyz, grad_vol):
     return vol.new_empty(vol.shape)
 
 
-@torch.library.custom_op("mvn_rocm::dlt_backward", mutates_args=())
+@_op("dlt_backward")
 def dlt_bwd(proj: Tensor, pts: Tensor, conf: Optional[Tensor], grad_out: Tensor) -> List[Tensor]:
     """-> [grad_pts (B,N,J,2), grad_conf (B,N,J) or empty]"""
     _require_gpu(proj, pts, conf, grad_out)
@@ -114,7 +114,7 @@ def unproject_backward(ctx, grad_out):
     want_conf = conf is not None and ctx.needs_input_grad[3]
     if not (ctx.needs_input_grad[0] or want_conf):
         return None, None, None, None, None, None, None
-    gfeat, gconf = unproject_bwd(feat, proj, coords, conf, grad_out, agg, align_corners, want_conf)
+    gfeat, gconf = call(unproject_bwd, feat, proj, coords, conf, grad_out, agg, align_corners, want_conf)
     return (gfeat if ctx.needs_input_grad[0] else None, None, None, gconf if want_conf else None,
             None, None, None)
 
@@ -125,7 +125,7 @@ def softargmax_backward(ctx, grad_xyz, grad_out):
     if not ctx.needs_input_grad[0]:
         return None, None, None, None, None, None
     gv = grad_out if (return_volume and grad_out is not None and grad_out.numel() > 0) else None
-    gin = softargmax3d_bwd(vol, coords, softmax, multiplier, grad_xyz, gv)
+    gin = call(softargmax3d_bwd, vol, coords, softmax, multiplier, grad_xyz, gv)
     return gin, None, None, None, None, None
 
 
@@ -134,7 +134,7 @@ def dlt_backward(ctx, grad_out):
     want_pts, want_conf = ctx.needs_input_grad[1], conf is not None and ctx.needs_input_grad[2]
     if not (want_pts or want_conf):
         return None, None, None
-    gpts, gconf = dlt_bwd(proj, pts, conf, grad_out)
+    gpts, gconf = call(dlt_bwd, proj, pts, conf, grad_out)
     return None, gpts if want_pts else None, gconf if want_conf else None
 
 

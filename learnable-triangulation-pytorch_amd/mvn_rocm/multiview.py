@@ -20,7 +20,9 @@ def triangulate_batch_of_points(proj_matricies_batch, points_batch, confidences_
     proj = proj_matricies_batch.float().contiguous()
     pts = points_batch.float().contiguous()
     conf = None if confidences_batch is None else confidences_batch.float().contiguous()
-    return DLTFunction.apply(proj, pts, conf)
+    if torch.is_grad_enabled() and (pts.requires_grad or (conf is not None and conf.requires_grad)):
+        return DLTFunction.apply(proj, pts, conf)
+    return _ops.call(_ops.dlt, proj, pts, conf)
 
 
 def triangulate_point_from_multiple_views_linear_torch(proj_matricies, points, confidences=None):
@@ -37,7 +39,7 @@ def triangulate_point_from_multiple_views_linear_torch(proj_matricies, points, c
 class DLTFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, proj, pts, conf):
-        out = _ops.dlt(proj, pts, conf)
+        out = _ops.call(_ops.dlt, proj, pts, conf)
         ctx.save_for_backward(proj, pts, conf)
         return out
 

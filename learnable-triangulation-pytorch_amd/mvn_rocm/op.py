@@ -28,6 +28,11 @@ def _is_cuboids(x) -> bool:
     return isinstance(x, Cuboids)
 
 
+def _needs_grad(*tensors) -> bool:
+    """Whether autograd must record the call (else the op runs without an autograd node)."""
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors)
+
+
 def _dtype_code(dtype: torch.dtype) -> int:
     if dtype == torch.float32:
         return _lib.MVN_DTYPE_F32
@@ -79,12 +84,16 @@ def unproject_heatmaps(heatmaps, proj_matricies, coord_volumes, volume_aggregati
             # in-kernel coordinates need the tiled kernel (N <= 8): materialise the volume
             coord_volumes, cub = cub.coord_volumes(), None
         else:
-            return UnprojectCuboidFunction.apply(feat, proj, cub.params, cub.volume_size, cub.transfer, conf, agg,
-                                                 bool(align_corners), od)
+            args = (feat, proj, cub.params, cub.volume_size, cub.transfer, conf, agg, bool(align_corners), od)
+            if _needs_grad(feat, conf):
+                return UnprojectCuboidFunction.apply(*args)
+            return _ops.call(_ops.unproject_cuboid, *args)
     coords = coord_volumes.float().contiguous()
     if coords.dim() != 5 or coords.shape[0] != feat.shape[0] or coords.shape[4] != 3:
         raise RuntimeError(f"coord_volumes must be (B, Vx, Vy, Vz, 3), got {tuple(coords.shape)}")
-    return UnprojectFunction.apply(feat, proj, coords, conf, agg, bool(align_corners), od)
+    if _needs_grad(feat, conf):
+        return UnprojectFunction.apply(feat, proj, coords, conf, agg, bool(align_corners), od)
+    return _ops.call(_ops.unproject, feat, proj, coords, conf, agg, bool(align_corners), od)
 
 
 def integrate_tensor_3d_with_coordinates(volumes, coord_volumes, softmax=True, *, multiplier=1.0,
@@ -108,13 +117,18 @@ def integrate_tensor_3d_with_coordinates(volumes, coord_volumes, softmax=True, *
         cub = coord_volumes
         if cub.shape != (vol.shape[0], Vx, Vy, Vz, 3):
             raise RuntimeError(f"cuboids {tuple(cub.shape)} do not match volumes {tuple(vol.shape)}")
-        xyz, out = SoftArgmaxCuboidFunction.apply(vol, cub.params, cub.volume_size, cub.transfer, bool(softmax),
-                                                  float(multiplier), bool(return_volumes), od)
+        if _needs_grad(vol):
+            xyz, out = SoftArgmaxCuboidFunction.apply(vol, cub.params, cub.volume_size, cub.transfer, bool(softmax),
+                                                      float(multiplier), bool(return_volumes), od)
+        else:
+            xyz, out = _ops.call(_ops.softargmax3d_cuboid, vol, cub.params, cub.transfer, bool(softmax),
+                                 float(multiplier), bool(return_volumes), od)
         return xyz, (out if return_volumes else None)
     coords = coord_volumes.float().contiguous()
     if coords.shape != (vol.shape[0], Vx, Vy, Vz, 3):
         raise RuntimeError(f"coord_volumes {tuple(coords.shape)} does not match volumes {tuple(vol.shape)}")
-    xyz, out = SoftArgmaxFunction.apply(vol, coords, bool(softmax), float(multiplier), bool(return_volumes), od)
+    args = (vol, coords, bool(softmax), float(multiplier), bool(return_volumes), od)
+    xyz, out = SoftArgmaxFunction.apply(*args) if _needs_grad(vol) else _ops.call(_ops.softargmax3d, *args)
     return xyz, (out if return_volumes else None)
 
 
@@ -133,7 +147,8 @@ def integrate_tensor_2d(heatmaps, softmax=True, *, multiplier=1.0, return_heatma
         raise RuntimeError(f"heatmaps must be (B, J, H, W), got {tuple(hm.shape)}")
     hm = hm.contiguous()
     od = _dtype_code(out_dtype if out_dtype is not None else hm.dtype)
-    xy, maps = SoftArgmax2dFunction.apply(hm, bool(softmax), float(multiplier), bool(return_heatmaps), od)
+    args = (hm, bool(softmax), float(multiplier), bool(return_heatmaps), od)
+    xy, maps = SoftArgmax2dFunction.apply(*args) if _needs_grad(hm) else _ops.call(_ops.softargmax2d, *args)
     return xy, (maps if return_heatmaps else None)
 
 
@@ -143,7 +158,7 @@ class UnprojectFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, feat, proj, coords, conf, agg, align_corners, out_dtype):
-        out = _ops.unproject(feat, proj, coords, conf, agg, align_corners, out_dtype)
+        out = _ops.call(_ops.unproject, feat, proj, coords, conf, agg, align_corners, out_dtype)
         ctx.save_for_backward(feat, proj, coords, conf)
         ctx.cfg = (agg, align_corners)
         return out
@@ -159,7 +174,7 @@ class SoftArgmaxFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, vol, coords, softmax, multiplier, return_volume, out_dtype):
-        xyz, out = _ops.softargmax3d(vol, coords, softmax, multiplier, return_volume, out_dtype)
+        xyz, out = _ops.call(_ops.softargmax3d, vol, coords, softmax, multiplier, return_volume, out_dtype)
         ctx.save_for_backward(vol, coords)
         ctx.cfg = (softmax, multiplier, return_volume)
         return xyz, out
@@ -177,7 +192,7 @@ class UnprojectCuboidFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, feat, proj, cub, V, transfer, conf, agg, align_corners, out_dtype):
-        out = _ops.unproject_cuboid(feat, proj, cub, V, transfer, conf, agg, align_corners, out_dtype)
+        out = _ops.call(_ops.unproject_cuboid, feat, proj, cub, V, transfer, conf, agg, align_corners, out_dtype)
         ctx.save_for_backward(feat, proj, cub, conf)
         ctx.cfg = (V, transfer, agg, align_corners)
         return out
@@ -192,7 +207,7 @@ class UnprojectCuboidFunction(torch.autograd.Function):
         if not (ctx.needs_input_grad[0] or want_conf):
             return (None,) * 9
         coords = Cuboids(cub, V, transfer).coord_volumes()
-        gfeat, gconf = _backward.unproject_bwd(feat, proj, coords, conf, grad_out, agg, align_corners, want_conf)
+        gfeat, gconf = _ops.call(_backward.unproject_bwd, feat, proj, coords, conf, grad_out, agg, align_corners, want_conf)
         return (gfeat if ctx.needs_input_grad[0] else None, None, None, None, None,
                 gconf if want_conf else None, None, None, None)
 
@@ -202,7 +217,7 @@ class SoftArgmaxCuboidFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, vol, cub, V, transfer, softmax, multiplier, return_volume, out_dtype):
-        xyz, out = _ops.softargmax3d_cuboid(vol, cub, transfer, softmax, multiplier, return_volume, out_dtype)
+        xyz, out = _ops.call(_ops.softargmax3d_cuboid, vol, cub, transfer, softmax, multiplier, return_volume, out_dtype)
         ctx.save_for_backward(vol, cub)
         ctx.cfg = (V, transfer, softmax, multiplier, return_volume)
         return xyz, out
@@ -217,7 +232,7 @@ class SoftArgmaxCuboidFunction(torch.autograd.Function):
             return (None,) * 8
         coords = Cuboids(cub, V, transfer).coord_volumes()
         gv = grad_out if (return_volume and grad_out is not None and grad_out.numel() > 0) else None
-        gin = _backward.softargmax3d_bwd(vol, coords, softmax, multiplier, grad_xyz, gv)
+        gin = _ops.call(_backward.softargmax3d_bwd, vol, coords, softmax, multiplier, grad_xyz, gv)
         return (gin,) + (None,) * 7
 
 
@@ -226,7 +241,7 @@ class SoftArgmax2dFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, hm, softmax, multiplier, return_maps, out_dtype):
-        xy, maps = _ops.softargmax2d(hm, softmax, multiplier, return_maps, out_dtype)
+        xy, maps = _ops.call(_ops.softargmax2d, hm, softmax, multiplier, return_maps, out_dtype)
         ctx.save_for_backward(hm, xy)
         ctx.cfg = (softmax, multiplier)
         return xy, maps

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One round's profiles (run on the GPU box):  tools/profile_round.sh <round-tag>
-#   1. rocprofv3 --kernel-trace --stats over bench.py (configs 2 and 3)
+#   1. rocprofv3 --kernel-trace --stats over bench.py (all configs; then configs 2, 3, 4 one per run)
 #   2. PMC HBM-traffic passes (FETCH_SIZE, WRITE_SIZE: separate passes) per config
 #   3. SQ instruction-mix passes on config 2
 # Raw output under gpurun_out/<tag>/; tools/profile_summary.py turns it into profiles/.
@@ -12,7 +12,14 @@ export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o kt -- \
     python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-in-kernel-coords > "$out/kt.log" 2>&1
 echo "kernel trace done"
-for cfg in 2 3; do
+# one config per process: a kernel that serves several configs gets one mean per config
+for cfg in 2 3 4; do
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt_cfg$cfg" -o kt -- \
+      python3 bench.py --config $cfg --steps 20 --warmup 5 --no-secondary --no-cpu-baseline \
+      > "$out/kt_cfg$cfg.log" 2>&1
+done
+echo "per-config kernel traces done"
+for cfg in 2 3 4; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex 'mvn' --output-format csv \
         -d "$out/pmc_${c}_cfg$cfg" -o pmc -- python3 tools/prof_unproject.py $cfg 5 > "$out/pmc_${c}_cfg$cfg.log" 2>&1

@@ -1,7 +1,8 @@
 """Turn tools/profile_round.sh output into the committed profiles/ files.
 
     python tools/profile_summary.py <round-tag>
-writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, mvn kernels), profiles/<tag>_traffic.json
+writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, mvn kernels; _cfgN: config N alone,
+with that run's bench line as <tag>_bench_cfgN_traced.json), profiles/<tag>_traffic.json
 (per config and kernel: mean FETCH_SIZE / WRITE_SIZE per dispatch; HBM bytes = 2 x FETCH + WRITE,
 MI355X_MICROARCH.md 'HBM': gfx950 FETCH_SIZE counts half the bytes of wide streaming reads) and
 profiles/<tag>_sq_cfg2.txt (SQ instruction mix of the unprojection).
@@ -26,19 +27,27 @@ def short(name):
     return name.split("(")[0]
 
 
-# 1. kernel stats
-stats = glob.glob(os.path.join(raw, "kt", "**", "*kernel_stats.csv"), recursive=True)
-rows = [r for f in stats for r in csv.DictReader(open(f))]
-with open(os.path.join(dst, f"{tag}_kernel_stats.csv"), "w", newline="") as fo:
-    w = csv.writer(fo)
-    w.writerow(["kernel", "calls", "avg_us", "min_us", "max_us", "pct_of_gpu_time"])
-    for r in rows:
-        w.writerow([short(r["Name"]), r["Calls"], f"{float(r['AverageNs']) / 1e3:.2f}",
-                    f"{float(r['MinNs']) / 1e3:.2f}", f"{float(r['MaxNs']) / 1e3:.2f}", r["Percentage"]])
+# 1. kernel stats: the whole bench, then one file per config (one config per traced process)
+for sub, suffix in (("kt", ""), ("kt_cfg2", "_cfg2"), ("kt_cfg3", "_cfg3"), ("kt_cfg4", "_cfg4")):
+    stats = glob.glob(os.path.join(raw, sub, "**", "*kernel_stats.csv"), recursive=True)
+    rows = [r for f in stats for r in csv.DictReader(open(f))]
+    if not rows:
+        continue
+    with open(os.path.join(dst, f"{tag}_kernel_stats{suffix}.csv"), "w", newline="") as fo:
+        w = csv.writer(fo)
+        w.writerow(["kernel", "calls", "avg_us", "min_us", "max_us", "pct_of_gpu_time"])
+        for r in rows:
+            w.writerow([short(r["Name"]), r["Calls"], f"{float(r['AverageNs']) / 1e3:.2f}",
+                        f"{float(r['MinNs']) / 1e3:.2f}", f"{float(r['MaxNs']) / 1e3:.2f}", r["Percentage"]])
+    log = os.path.join(raw, sub + ".log")
+    if suffix and os.path.exists(log):      # the traced run's own bench line
+        lines = [ln for ln in open(log) if ln.startswith("{")]
+        if lines:
+            open(os.path.join(dst, f"{tag}_bench{suffix}_traced.json"), "w").write(lines[-1])
 
 # 2. traffic
 traffic = {}
-for cfg in ("2", "3"):
+for cfg in ("2", "3", "4"):
     per = defaultdict(dict)
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         vals = defaultdict(list)

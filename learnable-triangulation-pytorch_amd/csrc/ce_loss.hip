@@ -18,8 +18,12 @@ namespace {
 
 constexpr int kBlock = 256;
 
+// torch.argmin's order: NaN below every number (a NaN distance wins; the first NaN among
+// several), then the smallest value, ties to the first index
 __device__ __forceinline__ void better(float& d, int& i, float d2, int i2) {
-  if (d2 < d || (d2 == d && i2 < i)) { d = d2; i = i2; }
+  const bool n = d != d, n2 = d2 != d2;
+  const bool take = n2 ? (!n || i2 < i) : (!n && (d2 < d || (d2 == d && i2 < i)));
+  if (take) { d = d2; i = i2; }
 }
 
 __global__ __launch_bounds__(kBlock) void nearest_voxel(const float* __restrict__ coords, const float* __restrict__ kps,
@@ -43,7 +47,7 @@ __global__ __launch_bounds__(kBlock) void nearest_voxel(const float* __restrict_
   __syncthreads();
   if (t == 0) {
     for (int w = 1; w < kBlock / kWave; ++w) better(best, bi, sd[w], si[w]);
-    out[bj] = (bi == INT_MAX) ? 0 : bi;             // all-NaN distances: voxel 0 (torch: NaN's index)
+    out[bj] = (bi == INT_MAX) ? 0 : bi;             // (every voxel is a candidate: bi < nvox)
   }
 }
 

@@ -24,6 +24,8 @@
 // in flight, XCD-balanced block order, buffer-descriptor stores — follows unproject_tiled.
 // Footprints that exceed one LDS buffer are staged in several passes of whole views;
 // a single view larger than a buffer sends its block to the global-gather fallback.
+#include <type_traits>
+
 #include "unproject_common.hpp"
 
 namespace mvn {
@@ -33,9 +35,30 @@ namespace {
 // Voxel tile per block and LDS image size.  Tiles short in z project more compactly:
 // footprint slots per voxel at the bench configs 2.2 (4x8x16), 1.7 (8x8x8), 2.2 (4x8x8);
 // the largest footprints 2,156 / 1,428 / 965 slots (tools: /tmp-free model in DESIGN.md).
+// NV views, G channels per LDS slot (16-byte slots of 4 f32 channels, or 8-byte slots of 2),
+// MC chunk slots per thread, WAVES waves per SIMD the register allocation must allow.
 template <int K> struct X4Shape;
-template <> struct X4Shape<0> { static constexpr int TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, MC = 2, WAVES = 4; };
-template <> struct X4Shape<2> { static constexpr int TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 1024, MC = 2, WAVES = 4; };
+template <> struct X4Shape<0> {   // 4 views, f32 maps
+  static constexpr int NV = 4, G = 4, TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, MC = 2, WAVES = 4;
+};
+template <> struct X4Shape<2> {   // 4 views, bf16 maps
+  static constexpr int NV = 4, G = 4, TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 1024, MC = 2, WAVES = 4;
+};
+// 8 views (BASELINE config 4, CMU-style): the footprint of 8 views doubles, so slots of 2
+// channels (8 bytes) keep two 2,048-slot buffers in 32 KiB (footprints of a 4x8x8 tile at
+// config 4: 1,170 slots mean, 1,897 max — tools/footprints.py); 8 views' per-voxel weights and
+// tap offsets (48 VGPRs) need the 168-register budget of 3 waves per SIMD (3 blocks per CU).
+template <> struct X4Shape<3> {
+  static constexpr int NV = 8, G = 2, TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 2048, MC = 3, WAVES = 3;
+};
+
+// LDS slot: one pixel's G channels as f32
+template <int G> struct SlotT;
+template <> struct SlotT<4> { using type = uint4; };
+template <> struct SlotT<2> { using type = uint2; };
+// channel pair q of a slot
+__device__ __forceinline__ f2 slot_pair(const uint4& s, int q) { return q ? hi2(s) : lo2(s); }
+__device__ __forceinline__ f2 slot_pair(const uint2& s, int) { return f2{__uint_as_float(s.x), __uint_as_float(s.y)}; }
 
 // Per-view LDS regions (block-uniform, scalar registers), packed 3 words per view —
 // (x0 + 1, y0 + 1), (bw, bh), sbase | cbase << 13 | pass << 24 — the derived fields
@@ -53,8 +76,8 @@ __device__ __forceinline__ Region make_region(int x0, int y0, int bw, int bh, in
   r.inv_cw = r.cw ? __builtin_amdgcn_rcpf(float(r.cw)) : 0.f;
   return r;
 }
-struct RegionSet {
-  uint32_t a[4], b[4], c[4];
+template <int NV> struct RegionSet {
+  uint32_t a[NV], b[NV], c[NV];
   __device__ __forceinline__ void set(int v, const Region& r) {
     a[v] = uint32_t(r.x0 + 1) | (uint32_t(r.y0 + 1) << 16);
     b[v] = uint32_t(r.bw) | (uint32_t(r.bh) << 16);
@@ -71,7 +94,7 @@ struct RegionSet {
   __device__ __forceinline__ Region pick(int u) const {
     uint32_t pa = a[0], pb = b[0], pc = c[0];
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
+    for (int k = 1; k < NV; ++k) {
       pa = u == k ? a[k] : pa;
       pb = u == k ? b[k] : pb;
       pc = u == k ? c[k] : pc;
@@ -85,17 +108,17 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ cub, int transfer, const float* __restrict__ conf, TOut* __restrict__ out, int B,
     int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, int budget, int out_cl) {
-  constexpr int NV = 4, G = 4;
   using S = X4Shape<K>;
+  constexpr int NV = S::NV, G = S::G, NP = G / 2;      // NP channel pairs per group
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ;
   constexpr int kThreads = S::THREADS, kBuf = S::SLOTS, MC = S::MC, kWaves = kThreads / kWave;
   static_assert(TX * TY * TZ == kThreads, "one voxel per thread");
   // per buffer: image slots [0, kTrash), 64 per-lane trash slots (the masked-off pixels of
   // a chunk are written there: no exec-mask branch per write), 2 zero slots
   constexpr int kZeroSlot = kBuf - 2, kTrash = kBuf - 2 - kWave;
-  // LDS slot = one pixel's G channels as f32 (16 bytes; bf16 maps are widened exactly when
-  // staged: bf16 slots halve the LDS bytes but the per-tap widening costs more VALU, r13)
-  using Slot = uint4;
+  // LDS slot = one pixel's G channels as f32 (16 / 8 bytes; bf16 maps are widened exactly
+  // when staged: bf16 slots halve the LDS bytes but the per-tap widening costs more VALU, r13)
+  using Slot = typename SlotT<G>::type;
   constexpr uint32_t kSlotB = sizeof(Slot);
   constexpr uint32_t E = sizeof(TIn);
 
@@ -189,49 +212,53 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   // ---- per-view boxes (ints, clipped to the pixels a tap can start at) ----------------
   int box[NV][4];
   {
-    // exact: every voxel's base pixel.  The 16 per-wave reductions (4 views x min x0, max x1,
+    // exact: every voxel's base pixel.  Per 4 views, the 16 per-wave reductions (min x0, max x1,
     // min y0, max y1; maxima as minima of negated values) run as one transposing butterfly:
     // lanes 32 apart swap halves of their 16 values (v_permlane32_swap), then rows 16 apart
     // (v_permlane16_swap), then lanes 8 and "4" apart (DPP row_ror:8, row_half_mirror) each
     // keep one of two, and the quads reduce — 35 instructions instead of 16 DPP reductions
     // with their readlanes.  Lane l ends with value (l >> 2) & 15 of the whole wave.
-    int q16[16];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      q16[4 * v + 0] = has[v] ? fx[v] : INT_MAX;
-      q16[4 * v + 1] = has[v] ? -fx[v] : INT_MAX;
-      q16[4 * v + 2] = has[v] ? fy[v] : INT_MAX;
-      q16[4 * v + 3] = has[v] ? -fy[v] : INT_MAX;
-    }
-    int q8[8], q4[4], q2[2];
+    for (int h = 0; h < NV / 4; ++h) {      // one butterfly per 4 views
+      int q16[16];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const auto r = __builtin_amdgcn_permlane32_swap(unsigned(q16[i]), unsigned(q16[8 + i]), false, false);
-      q8[i] = min(int(r[0]), int(r[1]));
-    }
+      for (int u = 0; u < 4; ++u) {
+        const int v = 4 * h + u;
+        q16[4 * u + 0] = has[v] ? fx[v] : INT_MAX;
+        q16[4 * u + 1] = has[v] ? -fx[v] : INT_MAX;
+        q16[4 * u + 2] = has[v] ? fy[v] : INT_MAX;
+        q16[4 * u + 3] = has[v] ? -fy[v] : INT_MAX;
+      }
+      int q8[8], q4[4], q2[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const auto r = __builtin_amdgcn_permlane16_swap(unsigned(q8[i]), unsigned(q8[4 + i]), false, false);
-      q4[i] = min(int(r[0]), int(r[1]));
-    }
-    const bool b3 = lane & 8, b2 = lane & 4;
+      for (int i = 0; i < 8; ++i) {
+        const auto r = __builtin_amdgcn_permlane32_swap(unsigned(q16[i]), unsigned(q16[8 + i]), false, false);
+        q8[i] = min(int(r[0]), int(r[1]));
+      }
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int send = b3 ? q4[m] : q4[m + 2], keep = b3 ? q4[m + 2] : q4[m];
-      q2[m] = min(keep, __builtin_amdgcn_update_dpp(INT_MAX, send, 0x128, 0xf, 0xf, false));   // row_ror:8
+      for (int i = 0; i < 4; ++i) {
+        const auto r = __builtin_amdgcn_permlane16_swap(unsigned(q8[i]), unsigned(q8[4 + i]), false, false);
+        q4[i] = min(int(r[0]), int(r[1]));
+      }
+      const bool b3 = lane & 8, b2 = lane & 4;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int send = b3 ? q4[m] : q4[m + 2], keep = b3 ? q4[m + 2] : q4[m];
+        q2[m] = min(keep, __builtin_amdgcn_update_dpp(INT_MAX, send, 0x128, 0xf, 0xf, false));   // row_ror:8
+      }
+      int q1;
+      {
+        const int send = b2 ? q2[0] : q2[1], keep = b2 ? q2[1] : q2[0];
+        q1 = min(keep, __builtin_amdgcn_update_dpp(INT_MAX, send, 0x141, 0xf, 0xf, false));     // row_half_mirror
+      }
+      q1 = min(q1, __builtin_amdgcn_update_dpp(INT_MAX, q1, 0xb1, 0xf, 0xf, false));              // quad_perm 1,0,3,2
+      q1 = min(q1, __builtin_amdgcn_update_dpp(INT_MAX, q1, 0x4e, 0xf, 0xf, false));              // quad_perm 2,3,0,1
+      if ((lane & 3) == 0) (&red[wid][4 * h][0])[(lane >> 2) & 15] = q1;
     }
-    int q1;
-    {
-      const int send = b2 ? q2[0] : q2[1], keep = b2 ? q2[1] : q2[0];
-      q1 = min(keep, __builtin_amdgcn_update_dpp(INT_MAX, send, 0x141, 0xf, 0xf, false));     // row_half_mirror
-    }
-    q1 = min(q1, __builtin_amdgcn_update_dpp(INT_MAX, q1, 0xb1, 0xf, 0xf, false));              // quad_perm 1,0,3,2
-    q1 = min(q1, __builtin_amdgcn_update_dpp(INT_MAX, q1, 0x4e, 0xf, 0xf, false));              // quad_perm 2,3,0,1
-    if ((lane & 3) == 0) (&red[wid][0][0])[(lane >> 2) & 15] = q1;
     __syncthreads();
     int part = INT_MAX;
     {
-      const int idx = lane & 15;
+      const int idx = lane & (4 * NV - 1);      // lane 4v+k reduces component k of view v
 #pragma unroll
       for (int q = 0; q < kWaves; ++q) part = min(part, (&red[q][0][0])[idx]);
     }
@@ -245,7 +272,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   }
 
   // ---- LDS regions (slots and chunks), in scalar registers ----------------------------
-  RegionSet rs;
+  RegionSet<NV> rs;
   int npass, total;
   {
     int snext = 0, cnext = 0, pass = 0, chunks0 = 0;
@@ -325,7 +352,11 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   auto write_group = [&](Slot* buf, const Chunk (&pre)[G], int s0, uint32_t mask) __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const Slot q = make_uint4(chunk_px(pre[0], p), chunk_px(pre[1], p), chunk_px(pre[2], p), chunk_px(pre[3], p));
+      Slot q;
+      if constexpr (G == 4)
+        q = make_uint4(chunk_px(pre[0], p), chunk_px(pre[1], p), chunk_px(pre[2], p), chunk_px(pre[3], p));
+      else
+        q = make_uint2(chunk_px(pre[0], p), chunk_px(pre[1], p));
       if constexpr (sizeof(TIn) == 2)
         buf[(mask & (1u << p)) ? s0 + p : kTrash + lane] = q;
       else if (mask & (1u << p))
@@ -334,7 +365,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   };
 
   // sample the views staged in an LDS buffer (all, or those of `pass`) into channel pairs
-  auto sample_views = [&](const char* buf, bool all, int pass, f2 (&sv)[2][NV]) __attribute__((always_inline)) {
+  auto sample_views = [&](const char* buf, bool all, int pass, f2 (&sv)[NP][NV]) __attribute__((always_inline)) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (!all && rs.get(v).pass != pass) continue;
@@ -343,8 +374,10 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       const Slot cq = *reinterpret_cast<const Slot*>(buf + asw[v]);
       const Slot d = *reinterpret_cast<const Slot*>(buf + asw[v] + kSlotB);
       const f2 w0 = splat<0>(wp[v][0]), w1 = splat<1>(wp[v][0]), w2 = splat<0>(wp[v][1]), w3 = splat<1>(wp[v][1]);
-      sv[0][v] = pk_fma(lo2(d), w3, pk_fma(lo2(cq), w2, pk_fma(lo2(bq), w1, lo2(a) * w0)));
-      sv[1][v] = pk_fma(hi2(d), w3, pk_fma(hi2(cq), w2, pk_fma(hi2(bq), w1, hi2(a) * w0)));
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+        sv[q][v] = pk_fma(slot_pair(d, q), w3,
+                          pk_fma(slot_pair(cq, q), w2, pk_fma(slot_pair(bq, q), w1, slot_pair(a, q) * w0)));
       if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight
     }
   };
@@ -352,9 +385,9 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   uint2 cl_buf[NG - 1];
 #pragma unroll
   for (int k = 0; k < NG - 1; ++k) cl_buf[k] = make_uint2(0u, 0u);
-  auto aggregate = [&](int c0, const f2 (&sv)[2][NV], float (&r)[G]) __attribute__((always_inline)) {
+  auto aggregate = [&](int c0, const f2 (&sv)[NP][NV], float (&r)[G]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < NP; ++q) {
       f2 cf[NV];
       if constexpr (AGG == MVN_AGG_CONF) {
 #pragma unroll
@@ -369,7 +402,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   // record (config 5).  bf16 NCDHW planes are direct 2-byte stores (r14: once the stores were
   // deferred past the next commit they beat 16-byte rows gathered through LDS, 542 -> 530 us).
   auto store_out = [&](int c0, const float (&r)[G]) __attribute__((always_inline)) {
-    if (out_cl) {
+    if constexpr (G == 4) if (out_cl) {      // (launch_x4 sends channels-last 8-view calls to the tiled kernel)
       // c0 is block-uniform; readfirstlane keeps it scalar (soffset operands must be SGPRs)
       const uint32_t soff = __builtin_amdgcn_readfirstlane(uint32_t(c0) * uint32_t(sizeof(TOut)));
       if constexpr (sizeof(TOut) == 2) {
@@ -414,7 +447,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       store_plane<TOut>(r[ch], ors, ooff, uint32_t(c0 + ch) * uint32_t(nvox) * uint32_t(sizeof(TOut)));
   };
   auto consume = [&](const Slot* buf, int c0, float (&r)[G]) __attribute__((always_inline)) {
-    f2 sv[2][NV];
+    f2 sv[NP][NV];
     sample_views(reinterpret_cast<const char*>(buf), true, 0, sv);
     aggregate(c0, sv, r);
     __builtin_amdgcn_sched_barrier(0);
@@ -478,7 +511,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   // ---- several passes of whole views per channel group (close cameras) ---------------
   tap_slots();
   for (int c0 = 0; c0 < C; c0 += G) {
-    f2 sv[2][NV];
+    f2 sv[NP][NV];
     for (int pass = 0; pass < npass; ++pass) {
 #pragma unroll
       for (int v = 0; v < NV; ++v) {          // every thread stages chunks of each view of the pass
@@ -512,22 +545,29 @@ template <int AGG, typename TIn, typename TOut>
 int launch_x4(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
               const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
               int align_corners, int out_cl, hipStream_t s) {
-  if (N != 4 || W % 4 != 0 || C % 4 != 0 || H > 32000 || W > 32000) return 1;
+  if (H > 32000 || W > 32000 || W % 4 != 0) return 1;
+  // 4 views: tile per input dtype (A/B at the bench configs), f32 4x8x16,
+  // bf16 4x8x8; 8 views: 2-channel slots, NCDHW output only
+  const bool four = N == 4 && C % 4 == 0, eight = N == 8 && C % 2 == 0 && !out_cl;
+  if (!four && !eight) return 1;
   if ((long long)N * C * H * W * sizeof(TIn) >= (1LL << 31) ||
       (long long)C * Vx * Vy * Vz * sizeof(TOut) >= (1LL << 31))
     return MVN_ERR_SHAPE;
   const int knob = unproject_lds_slot_budget();
   const int budget = knob > 0 ? knob : 1 << 30;
-  // tile per input dtype (A/B at the bench configs): f32 4x8x16, bf16 4x8x8
-  constexpr int K = sizeof(TIn) == 2 ? 2 : 0;
-  using S = X4Shape<K>;
-  const long long nb = (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) *
-                       ((Vz + S::TZ - 1) / S::TZ);
-  if (nb > INT_MAX) return MVN_ERR_SHAPE;
-  unproject_x4<AGG, TIn, TOut, K><<<int(nb), S::THREADS, 0, s>>>(
-      static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, C, H, W, Vx, Vy,
-      Vz, align_corners, budget, out_cl);
-  return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
+  auto go = [&](auto shape) {
+    constexpr int K = decltype(shape)::value;
+    using S = X4Shape<K>;
+    const long long nb = (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) *
+                         ((Vz + S::TZ - 1) / S::TZ);
+    if (nb > INT_MAX) return MVN_ERR_SHAPE;
+    unproject_x4<AGG, TIn, TOut, K><<<int(nb), S::THREADS, 0, s>>>(
+        static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, C, H, W, Vx, Vy,
+        Vz, align_corners, budget, out_cl);
+    return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
+  };
+  if (eight) return go(std::integral_constant<int, 3>{});
+  return go(std::integral_constant<int, sizeof(TIn) == 2 ? 2 : 0>{});
 }
 
 // Diagnostics (mvn_debug_unproject_occupancy): resident blocks per CU of the softmax kernels.

@@ -99,7 +99,8 @@ def coord_volumes(base_points, cuboid_side, volume_size, thetas, kind="coco", tr
 def nearest_voxel(coords, keypoints):
     """(B,Vx,Vy,Vz,3), (B,J,3) -> (B,J) flat index of the nearest voxel (loss.py:63-66):
     f32 squared distance summed x, y, z in order, its IEEE square root, argmin with the
-    first index on ties (distinct squared distances can round to one root)."""
+    first index on ties (distinct squared distances can round to one root).  NaN distances:
+    numpy's argmin, like torch.argmin, returns the first NaN's index."""
     f = np.float32
     c = np.asarray(coords, f).reshape(len(coords), -1, 3)
     k = np.asarray(keypoints, f)

@@ -256,6 +256,22 @@ def test_nearest_voxel_sqrt_tie_takes_first_index(device):
     assert int(idx[0, 0]) == 0
 
 
+def test_nearest_voxel_nan_distance_wins_like_argmin(device):
+    """torch.argmin (loss.py:66) treats NaN as the minimum and returns the FIRST NaN's index:
+    a NaN voxel coordinate (or keypoint) beats every finite distance."""
+    from mvn_rocm import loss as mloss
+    rng = np.random.default_rng(80)
+    coords = rng.uniform(-100, 100, (2, 4, 4, 4, 3)).astype(np.float32)
+    coords.reshape(2, -1, 3)[0, 37, 1] = np.nan
+    coords.reshape(2, -1, 3)[0, 50, 0] = np.nan
+    kps = rng.uniform(-100, 100, (2, 3, 3)).astype(np.float32)
+    kps[1, 2, 2] = np.nan                                    # every distance of this joint NaN
+    ref = restate_np.nearest_voxel(coords, kps)
+    assert (ref[0] == 37).all() and ref[1, 2] == 0
+    idx = mloss.nearest_voxel(_t(coords, device), _t(kps, device))
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+
+
 # ----------------------------------------------------------------------------- C ABI reentrancy
 def test_c_abi_two_threads_two_streams(device):
     """§8b Threading: the C entry points are reentrant — two host threads launching on two

@@ -1,5 +1,5 @@
-"""The four-view unprojection kernel (csrc/unproject_x4.hip: chunked staging, packed f32
-arithmetic) against the generic tiled kernel (bit for bit, every aggregation, dtype and
+"""The chunk-staged unprojection kernel (csrc/unproject_x4.hip: chunked staging, packed f32
+arithmetic; 4 views with 4-channel LDS slots, 8 views with 2-channel slots) against the generic tiled kernel (bit for bit, every aggregation, dtype and
 layout) and against the C oracle, on every staging path (one LDS pass, several passes,
 global-gather fallback) and on coordinate volumes that are not affine grids.  MI355X only."""
 import numpy as np
@@ -24,17 +24,23 @@ def _run(vb_feat, proj, coords, method, conf, out_dtype=None, **knobs):
         return op.unproject_heatmaps(vb_feat, proj, coords, method, conf, out_dtype=out_dtype)
 
 
-def _batch(device, seed, heatmap=64, volume=32, channels=8, dtype=torch.float32):
+def _batch(device, seed, heatmap=64, volume=32, channels=8, dtype=torch.float32, n_views=4):
     from mvn_rocm import synth
-    vb = synth.volumetric_batch(2, n_views=4, channels=channels, heatmap=heatmap, volume=volume, seed=seed)
-    conf = torch.from_numpy(np.random.default_rng(seed).uniform(0.05, 1.0, (2, 4, channels)).astype(np.float32))
+    vb = synth.volumetric_batch(2, n_views=n_views, channels=channels, heatmap=heatmap, volume=volume, seed=seed)
+    conf = torch.from_numpy(np.random.default_rng(seed).uniform(0.05, 1.0, (2, n_views, channels)).astype(np.float32))
     return vb, conf
 
 
+# (views, channels): 4 views / 4-channel slots; 8 views / 2-channel slots, also with a channel
+# count that is not a multiple of 4
+VIEWS = ((4, 8), (8, 8), (8, 6))
+
+
+@pytest.mark.parametrize("views", VIEWS, ids=lambda v: f"{v[0]}v{v[1]}c")
 @pytest.mark.parametrize("method", METHODS)
 @pytest.mark.parametrize("dt", ("f32", "bf16", "bf16->f32"))
-def test_x4_equals_generic_kernel_and_oracle(device, method, dt):
-    vb, conf = _batch(device, 70)
+def test_x4_equals_generic_kernel_and_oracle(device, method, dt, views):
+    vb, conf = _batch(device, 70, n_views=views[0], channels=views[1])
     feat = vb.features.to(device)
     od = None
     if dt != "f32":
@@ -61,13 +67,15 @@ def _tile_areas(proj, coords, H, W, tile=(4, 8, 16)):
     return tile_footprints(proj, coords, H, W, tile)
 
 
+@pytest.mark.parametrize("n_views", (4, 8))
 @pytest.mark.parametrize("path", ("multipass", "fallback"))
 @pytest.mark.parametrize("method", ("sum", "softmax"))
-def test_x4_staging_paths(device, path, method):
+def test_x4_staging_paths(device, path, method, n_views):
     """LDS budgets that force several staging passes of whole views, and single views
     larger than the budget (global-gather fallback) — against the oracle."""
-    vb, conf = _batch(device, 71, heatmap=64, volume=32, channels=8)
-    areas = _tile_areas(vb.proj.numpy(), vb.coords.numpy(), 64, 64)
+    vb, conf = _batch(device, 71, heatmap=64, volume=32, channels=8, n_views=n_views)
+    tile = (4, 8, 16) if n_views == 4 else (4, 8, 8)
+    areas = _tile_areas(vb.proj.numpy(), vb.coords.numpy(), 64, 64, tile)
     if path == "multipass":
         budget = int(areas.max()) + 64
         assert (areas.sum(1) + 1 > budget).any()
@@ -82,11 +90,12 @@ def test_x4_staging_paths(device, path, method):
         np.testing.assert_array_equal(out.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("n_views", (4, 8))
 @pytest.mark.parametrize("method", ("sum", "softmax"))
-def test_x4_non_affine_coordinates(device, method):
+def test_x4_non_affine_coordinates(device, method, n_views):
     """op.py:99 accepts ANY coordinate volume: jittered and shuffled voxel coordinates (not
     an affine grid) must still match the oracle."""
-    vb, _ = _batch(device, 72, heatmap=64, volume=32, channels=8)
+    vb, _ = _batch(device, 72, heatmap=64, volume=32, channels=8, n_views=n_views)
     rng = np.random.default_rng(72)
     X = vb.coords.numpy().copy()
     X += rng.normal(0, 40.0, X.shape).astype(np.float32)               # jitter (~1 voxel)
@@ -120,13 +129,14 @@ def test_x4_channels_last_and_cuboids_equal_generic(device, dt, channels):
     assert torch.equal(_bits(a), _bits(b))
 
 
+@pytest.mark.parametrize("n_views", (4, 8))
 @pytest.mark.parametrize("method", METHODS)
 @pytest.mark.parametrize("dt", ("f32", "bf16", "bf16->f32"))
-def test_x4_partial_tiles(device, method, dt):
+def test_x4_partial_tiles(device, method, dt, n_views):
     """A volume that is not a multiple of either tile (20 x 28 x 36 of a 40^3 grid): edge
-    tiles with inactive voxels (bf16 output then skips the LDS-gathered rows) next to full
-    ones — bitwise against the generic kernel, and against the oracle."""
-    vb, conf = _batch(device, 74, heatmap=64, volume=40, channels=8)
+    tiles with inactive voxels next to full ones — bitwise against the generic kernel, and
+    against the oracle."""
+    vb, conf = _batch(device, 74, heatmap=64, volume=40, channels=8, n_views=n_views)
     X = vb.coords[:, 2:22, 5:33, 1:37].contiguous()
     feat = vb.features.to(device)
     od = None

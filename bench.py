@@ -201,9 +201,9 @@ def measured_traffic(cfg_name):
 def kernel_name(c):
     import torch
     t = "float" if c["dtype"] == torch.float32 else "bf16"
-    if c["views"] == 4:      # the four-view kernel (csrc/unproject_x4.hip), tile per dtype
+    if c["views"] == 4:      # the chunk-staged kernel (csrc/unproject_x4.hip), tile per dtype
         return f"unproject_x4<softmax, {t}, {t}, tile {'4x8x16' if t == 'float' else '4x8x8'}>"
-    return f"unproject_tiled<softmax, {t}, {t}, 8 views>"
+    return f"unproject_x4<softmax, {t}, {t}, 8 views, 2-channel slots, tile 4x8x8>"
 
 
 def dtype_name(dt):

@@ -347,8 +347,9 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
 #pragma unroll
     for (int k = 0; k < G; ++k) pre[k] = load_chunk<TIn>(frs, goff, uint32_t((c0 + k) * HW) * E);
   };
-  // masked-off pixels: bf16 maps write them to the lane's trash slot (no exec-mask branch
-  // per write), f32 maps branch (A/B at the bench configs: each is the faster for its dtype)
+  // masked-off pixels: bf16 maps and 2-channel slots write them to the lane's trash slot
+  // (no exec-mask branch per write), f32 maps on 4-channel slots branch (A/B at the bench
+  // configs: each is the faster for its case; 8 views 694 -> 677 us, r16)
   auto write_group = [&](Slot* buf, const Chunk (&pre)[G], int s0, uint32_t mask) __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -357,22 +358,37 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
         q = make_uint4(chunk_px(pre[0], p), chunk_px(pre[1], p), chunk_px(pre[2], p), chunk_px(pre[3], p));
       else
         q = make_uint2(chunk_px(pre[0], p), chunk_px(pre[1], p));
-      if constexpr (sizeof(TIn) == 2)
+      if constexpr (sizeof(TIn) == 2 || G == 2)
         buf[(mask & (1u << p)) ? s0 + p : kTrash + lane] = q;
       else if (mask & (1u << p))
         buf[s0 + p] = q;
     }
   };
 
+  // one tap's slot.  8-byte slots are read as single ds_read_b64 (2 LDS cycles, 64 banks):
+  // left to itself the compiler pairs the two taps of a row into ds_read2_b64, which the
+  // LDS services as two 16-lane-group accesses at half the rate (8 cycles, 32 banks) —
+  // config 4: 774 -> 694 us (r16).  A volatile LDS load is not merged; its order relative
+  // to the other taps is the program order anyway.
+  auto tap = [&](const char* p) __attribute__((always_inline)) -> Slot {
+    if constexpr (G == 2) {
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      typedef const volatile __attribute__((address_space(3))) u32x2* lds_ptr;
+      const u32x2 q = *(lds_ptr)(p);
+      return make_uint2(q.x, q.y);
+    } else {
+      return *reinterpret_cast<const Slot*>(p);
+    }
+  };
   // sample the views staged in an LDS buffer (all, or those of `pass`) into channel pairs
   auto sample_views = [&](const char* buf, bool all, int pass, f2 (&sv)[NP][NV]) __attribute__((always_inline)) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (!all && rs.get(v).pass != pass) continue;
-      const Slot a = *reinterpret_cast<const Slot*>(buf + anw[v]);
-      const Slot bq = *reinterpret_cast<const Slot*>(buf + anw[v] + kSlotB);
-      const Slot cq = *reinterpret_cast<const Slot*>(buf + asw[v]);
-      const Slot d = *reinterpret_cast<const Slot*>(buf + asw[v] + kSlotB);
+      const Slot a = tap(buf + anw[v]);
+      const Slot bq = tap(buf + anw[v] + kSlotB);
+      const Slot cq = tap(buf + asw[v]);
+      const Slot d = tap(buf + asw[v] + kSlotB);
       const f2 w0 = splat<0>(wp[v][0]), w1 = splat<1>(wp[v][0]), w2 = splat<0>(wp[v][1]), w3 = splat<1>(wp[v][1]);
 #pragma unroll
       for (int q = 0; q < NP; ++q)

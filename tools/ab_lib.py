@@ -32,6 +32,8 @@ def main():
     cases = [(8, 4, torch.float32, "cfg2 f32 B=8"), (32, 4, torch.bfloat16, "cfg3 bf16 B=32")]
     if os.environ.get("AB_CFG4"):
         cases.append((16, 8, torch.float32, "cfg4 f32 N=8 B=16"))
+    if os.environ.get("AB_ONLY"):        # e.g. AB_ONLY=cfg4
+        cases = [c for c in cases if c[3].startswith(os.environ["AB_ONLY"])]
     for B, NV, dt, label in cases:
         vb = synth.volumetric_batch(B, n_views=NV, dtype=dt, device=dev, seed=0)
         feat, proj, coords = vb.features, vb.proj, vb.coords

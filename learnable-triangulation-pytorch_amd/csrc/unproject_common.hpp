@@ -373,12 +373,14 @@ __device__ __forceinline__ f2 aggregate_pair(const f2 (&s)[NV], const f2 (&cf)[N
 // (whole step at config 2: 261.5 -> 257.8 us); 2-byte bf16 stores must not (577 -> 1,664 us).
 constexpr int kStorePolicyF32 = 2;     // nt
 constexpr int kStorePolicyBf16 = 0;    // default
-template <typename T> __device__ __forceinline__ void store_plane(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s);
-template <> __device__ __forceinline__ void store_plane<float>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, kStorePolicyF32);
-}
-template <> __device__ __forceinline__ void store_plane<uint16_t>(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
-  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, kStorePolicyBf16);
+// POL_F32: the f32 store's cache policy (the non-temporal default suits 64-byte z-runs;
+// 32-byte runs, whose lines several blocks complete, merge better through L2 with 0)
+template <typename T, int POL_F32 = kStorePolicyF32>
+__device__ __forceinline__ void store_plane(float x, __amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+  if constexpr (sizeof(T) == 4)
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, v, s, POL_F32);
+  else
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)), r, v, s, kStorePolicyBf16);
 }
 
 // Per-view region of the LDS image (block-uniform, SGPRs).

@@ -38,18 +38,24 @@ namespace {
 // NV views, G channels per LDS slot (16-byte slots of 4 f32 channels, or 8-byte slots of 2),
 // MC chunk slots per thread, WAVES waves per SIMD the register allocation must allow.
 template <int K> struct X4Shape;
+// STORE_F32: cache policy of f32 output stores (non-temporal for 64-byte z-runs).
 template <> struct X4Shape<0> {   // 4 views, f32 maps
   static constexpr int NV = 4, G = 4, TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, MC = 2, WAVES = 4;
+  static constexpr int STORE_F32 = kStorePolicyF32;
 };
 template <> struct X4Shape<2> {   // 4 views, bf16 maps
   static constexpr int NV = 4, G = 4, TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 1024, MC = 2, WAVES = 4;
+  static constexpr int STORE_F32 = kStorePolicyF32;
 };
 // 8 views (BASELINE config 4, CMU-style): the footprint of 8 views doubles, so slots of 2
 // channels (8 bytes) keep two 2,048-slot buffers in 32 KiB (footprints of a 4x8x8 tile at
 // config 4: 1,170 slots mean, 1,897 max — tools/footprints.py); 8 views' per-voxel weights and
 // tap offsets (48 VGPRs) need the 168-register budget of 3 waves per SIMD (3 blocks per CU).
+// f32 output: the tile's 32-byte z-runs leave through L2 with the default policy (4 blocks
+// complete each 128-byte line; non-temporal stores wrote 1.47x the output, 686 -> 647 us, r16).
 template <> struct X4Shape<3> {
   static constexpr int NV = 8, G = 2, TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 2048, MC = 3, WAVES = 3;
+  static constexpr int STORE_F32 = 0;
 };
 
 // LDS slot: one pixel's G channels as f32
@@ -460,7 +466,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     }
 #pragma unroll
     for (int ch = 0; ch < G; ++ch)
-      store_plane<TOut>(r[ch], ors, ooff, uint32_t(c0 + ch) * uint32_t(nvox) * uint32_t(sizeof(TOut)));
+      store_plane<TOut, S::STORE_F32>(r[ch], ors, ooff, uint32_t(c0 + ch) * uint32_t(nvox) * uint32_t(sizeof(TOut)));
   };
   auto consume = [&](const Slot* buf, int c0, float (&r)[G]) __attribute__((always_inline)) {
     f2 sv[NP][NV];

@@ -1,5 +1,6 @@
-// Four-view unprojection for gfx950 — the production kernel behind mvn_unproject for the
-// configurations of BASELINE.json (4 views, W % 4 == 0, C % 4 == 0).
+// Chunk-staged unprojection for gfx950 — the production kernel behind mvn_unproject for the
+// configurations of BASELINE.json: 4 views (W % 4 == 0, C % 4 == 0; 16-byte LDS slots of 4
+// channels) and 8 views (config 4: W % 4 == 0, C % 2 == 0, NCDHW; 8-byte slots of 2).
 //
 // Contract and numerics: mvn/utils/op.py:99-163 exactly as unproject_tiled.hip (sum / max /
 // conf bit-exact with the reference; softmax max-first with exp2 and one reciprocal, same

@@ -19,13 +19,15 @@ __device__ __forceinline__ float softmax_exp(float s, float ml) {   // ml = m * 
   return __builtin_amdgcn_exp2f(__builtin_fmaf(s, kLog2e, -ml));
 }
 
-// Bilinear taps of one voxel in one view: 4 clamped plane offsets + 4 weights.
-// Out-of-bounds corners and invalid (behind-camera) voxels get weight 0, which is
-// bit-identical to the reference's zero-valued corner / zeroed sample for finite
-// feature values (fma(v, 0, acc) == acc).
+// Bilinear taps of one voxel in one view: 4 clamped plane offsets + 4 weights + the mask
+// of corners inside the image.  Out-of-bounds corners read the value 0 (grid_sample's
+// padding_mode='zeros': the corner VALUE is zero, so its product is +0 whatever the sign
+// of the clamped pixel) and, like every corner of an invalid (behind-camera) voxel, carry
+// weight 0 (0 * 0: no NaN from the weights of far-off or non-finite coordinates).
 struct Taps {
   int o0, o1, o2, o3;
   float w0, w1, w2, w3;
+  unsigned in;        // bit k: corner k (nw, ne, sw, se) inside the image, voxel valid
 };
 
 // Continuous grid_sample pixel coordinate of one voxel in one view, plus the depth mask.
@@ -141,19 +143,21 @@ __device__ __forceinline__ Taps view_taps(const float* __restrict__ Pv, float x,
   const int x0 = x0in ? int(fx0) : 0, x1 = x1in ? int(fx0) + 1 : 0;
   const int y0 = y0in ? int(fy0) : 0, y1 = y1in ? int(fy0) + 1 : 0;
   Taps t;
-  t.o0 = y0 * W + x0;  t.w0 = (ok & y0in & x0in) ? sy * sx : 0.f;   // nw
-  t.o1 = y0 * W + x1;  t.w1 = (ok & y0in & x1in) ? sy * tx : 0.f;   // ne
-  t.o2 = y1 * W + x0;  t.w2 = (ok & y1in & x0in) ? ty * sx : 0.f;   // sw
-  t.o3 = y1 * W + x1;  t.w3 = (ok & y1in & x1in) ? ty * tx : 0.f;   // se
+  const bool i0 = ok & y0in & x0in, i1 = ok & y0in & x1in, i2 = ok & y1in & x0in, i3 = ok & y1in & x1in;
+  t.o0 = y0 * W + x0;  t.w0 = i0 ? sy * sx : 0.f;   // nw
+  t.o1 = y0 * W + x1;  t.w1 = i1 ? sy * tx : 0.f;   // ne
+  t.o2 = y1 * W + x0;  t.w2 = i2 ? ty * sx : 0.f;   // sw
+  t.o3 = y1 * W + x1;  t.w3 = i3 ? ty * tx : 0.f;   // se
+  t.in = (i0 ? 1u : 0u) | (i1 ? 2u : 0u) | (i2 ? 4u : 0u) | (i3 ? 8u : 0u);
   return t;
 }
 
 template <typename TIn>
 __device__ __forceinline__ float sample(const TIn* __restrict__ plane, const Taps& t) {
-  const float a = to_f32(plane[t.o0]);
-  const float b = to_f32(plane[t.o1]);
-  const float c = to_f32(plane[t.o2]);
-  const float d = to_f32(plane[t.o3]);
+  const float a = (t.in & 1u) ? to_f32(plane[t.o0]) : 0.f;
+  const float b = (t.in & 2u) ? to_f32(plane[t.o1]) : 0.f;
+  const float c = (t.in & 4u) ? to_f32(plane[t.o2]) : 0.f;
+  const float d = (t.in & 8u) ? to_f32(plane[t.o3]) : 0.f;
   return __builtin_fmaf(d, t.w3, __builtin_fmaf(c, t.w2, __builtin_fmaf(b, t.w1, a * t.w0)));
 }
 

@@ -21,8 +21,10 @@
 #define AGG_SOFTMAX 2
 #define AGG_CONF 3
 
-/* One bilinear tap set; zero-valued corners are modelled by zero weights. */
-typedef struct { long o[4]; float w[4]; } taps_t;
+/* One bilinear tap set.  A corner outside the image reads the VALUE 0 (padding_mode
+ * 'zeros'; torch's grid_sample gives +0 there whatever the sign of the nearest pixel) and
+ * also carries weight 0 (as every corner of an invalid voxel), so its product is +0. */
+typedef struct { long o[4]; float w[4]; int in[4]; } taps_t;
 
 /* mvn/utils/op.py:117-134: projection (multiview.py:80-101 via the K=4 sgemm of
  * multiview.py:96), depth mask (op.py:121), divide guard (op.py:123), dehomogenise
@@ -53,10 +55,12 @@ static taps_t view_taps(const float *Pv, float x, float y, float z, int H, int W
     int y0in = fy0 >= 0.f && fy0 < (float)H, y1in = fy0 >= -1.f && fy0 < (float)(H - 1);
     long x0 = x0in ? (long)fx0 : 0, x1 = x1in ? (long)fx0 + 1 : 0;
     long y0 = y0in ? (long)fy0 : 0, y1 = y1in ? (long)fy0 + 1 : 0;
-    t.o[0] = y0 * W + x0; t.w[0] = (!invalid && y0in && x0in) ? sy * sx : 0.f;
-    t.o[1] = y0 * W + x1; t.w[1] = (!invalid && y0in && x1in) ? sy * tx : 0.f;
-    t.o[2] = y1 * W + x0; t.w[2] = (!invalid && y1in && x0in) ? ty * sx : 0.f;
-    t.o[3] = y1 * W + x1; t.w[3] = (!invalid && y1in && x1in) ? ty * tx : 0.f;
+    t.in[0] = !invalid && y0in && x0in; t.in[1] = !invalid && y0in && x1in;
+    t.in[2] = !invalid && y1in && x0in; t.in[3] = !invalid && y1in && x1in;
+    t.o[0] = y0 * W + x0; t.w[0] = t.in[0] ? sy * sx : 0.f;
+    t.o[1] = y0 * W + x1; t.w[1] = t.in[1] ? sy * tx : 0.f;
+    t.o[2] = y1 * W + x0; t.w[2] = t.in[2] ? ty * sx : 0.f;
+    t.o[3] = y1 * W + x1; t.w[3] = t.in[3] ? ty * tx : 0.f;
     return t;
 }
 
@@ -69,13 +73,15 @@ static float bf16_to_f32(uint16_t h) {
 
 /* ATen CPU grid sampler combination order. */
 static float sample_plane(const float *plane, const taps_t *t) {
-    return fmaf(plane[t->o[3]], t->w[3], fmaf(plane[t->o[2]], t->w[2],
-                fmaf(plane[t->o[1]], t->w[1], plane[t->o[0]] * t->w[0])));
+    float v[4];
+    for (int k = 0; k < 4; ++k) v[k] = t->in[k] ? plane[t->o[k]] : 0.f;
+    return fmaf(v[3], t->w[3], fmaf(v[2], t->w[2], fmaf(v[1], t->w[1], v[0] * t->w[0])));
 }
 
 static float sample_plane_bf16(const uint16_t *plane, const taps_t *t) {
-    return fmaf(bf16_to_f32(plane[t->o[3]]), t->w[3], fmaf(bf16_to_f32(plane[t->o[2]]), t->w[2],
-                fmaf(bf16_to_f32(plane[t->o[1]]), t->w[1], bf16_to_f32(plane[t->o[0]]) * t->w[0])));
+    float v[4];
+    for (int k = 0; k < 4; ++k) v[k] = t->in[k] ? bf16_to_f32(plane[t->o[k]]) : 0.f;
+    return fmaf(v[3], t->w[3], fmaf(v[2], t->w[2], fmaf(v[1], t->w[1], v[0] * t->w[0])));
 }
 
 /* mvn/utils/op.py:99-163 unproject_heatmaps.  feat is f32 (feat_bf16 == 0) or raw bf16

@@ -33,6 +33,17 @@ def device():
     return torch.device("cuda:0")
 
 
+def assert_bits_equal(a, b):
+    """float32 arrays equal bit for bit: unlike assert_array_equal, +0 vs -0 (and NaN
+    payloads) count as differences — grid_sample's zero padding yields +0, and a kernel that
+    multiplies a clamped negative pixel by a zero weight yields -0."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    bad = a.view(np.uint32) != b.view(np.uint32)
+    assert not bad.any(), f"{int(bad.sum())} of {bad.size} elements differ in their bits (first: {a[bad][:4]} vs {b[bad][:4]})"
+
+
 def max_rel(a, b):
     """max |a - b| / max |b| (SURVEY.md §8d parity metric)."""
     a = np.asarray(a, np.float64)

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import max_rel
+from conftest import assert_bits_equal, max_rel
 from oracle import capi, restate_np
 
 pytestmark = pytest.mark.gpu
@@ -57,7 +57,7 @@ def test_cfg3_bf16_unproject_full_size_vs_oracle(device, method):
     if method == "softmax":
         assert max_rel(out32.cpu().numpy(), ref) <= 1e-5
     else:
-        np.testing.assert_array_equal(out32.cpu().numpy(), ref)
+        assert_bits_equal(out32.cpu().numpy(), ref)
     out16 = op.unproject_heatmaps(vb.features, vb.proj, vb.coords, method)
     assert out16.dtype == torch.bfloat16
     assert_within_one_bf16_ulp(out16, ref, 1e-5 * np.abs(ref).max() if method == "softmax" else 0.0)
@@ -107,7 +107,7 @@ def test_cfg4_eight_views_full_size_vs_oracle(device, method):
     if method == "softmax":
         assert max_rel(out.cpu().numpy(), ref) <= 1e-5
     else:
-        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+        assert_bits_equal(out.cpu().numpy(), ref)
     assert 0.2 < (ref != 0).mean()
 
 

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import max_rel
+from conftest import assert_bits_equal, max_rel
 from oracle import capi, restate_np
 
 pytestmark = pytest.mark.gpu
@@ -53,7 +53,7 @@ def test_unproject_cuboid_is_bit_identical_to_the_volume_path(device, n_views, m
         if method == "softmax":
             assert max_rel(a.cpu().numpy(), ref) <= 1e-5
         else:
-            np.testing.assert_array_equal(a.cpu().numpy(), ref)
+            assert_bits_equal(a.cpu().numpy(), ref)
 
 
 def test_unproject_cuboid_bf16_and_every_kernel_path(device):

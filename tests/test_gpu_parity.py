@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import max_rel
+from conftest import assert_bits_equal, max_rel
 from oracle import capi, restate_np
 
 pytestmark = pytest.mark.gpu
@@ -37,8 +37,8 @@ def bf16_to_f32(bits):
 def assert_unproject_parity(out, ref, method, tol=1e-5):
     if method == "softmax":
         assert max_rel(out, ref) <= tol
-    else:
-        np.testing.assert_array_equal(out, ref)
+    else:                       # bit for bit, signed zeros included
+        assert_bits_equal(out, ref)
 
 
 # ----------------------------------------------------------------------------- unproject

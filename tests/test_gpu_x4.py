@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import max_rel
+from conftest import assert_bits_equal, max_rel
 from oracle import capi
 
 pytestmark = pytest.mark.gpu
@@ -59,7 +59,7 @@ def test_x4_equals_generic_kernel_and_oracle(device, method, dt, views):
     elif method == "softmax":
         assert max_rel(got, ref) <= 1e-5
     else:
-        np.testing.assert_array_equal(got, ref)
+        assert_bits_equal(got, ref)
 
 
 def _tile_areas(proj, coords, H, W, tile=(4, 8, 16)):
@@ -87,7 +87,7 @@ def test_x4_staging_paths(device, path, method, n_views):
     if method == "softmax":
         assert max_rel(out.cpu().numpy(), ref) <= 1e-5
     else:
-        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+        assert_bits_equal(out.cpu().numpy(), ref)
 
 
 @pytest.mark.parametrize("n_views", (4, 8))
@@ -108,7 +108,7 @@ def test_x4_non_affine_coordinates(device, method, n_views):
     if method == "softmax":
         assert max_rel(out.cpu().numpy(), ref) <= 1e-5
     else:
-        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+        assert_bits_equal(out.cpu().numpy(), ref)
 
 
 @pytest.mark.parametrize("channels", (32, 12, 20))
@@ -157,7 +157,7 @@ def test_x4_partial_tiles(device, method, dt, n_views):
     elif method == "softmax":
         assert max_rel(got, ref) <= 1e-5
     else:
-        np.testing.assert_array_equal(got, ref)
+        assert_bits_equal(got, ref)
 
 
 @pytest.mark.parametrize("dt", ("f32", "bf16"))
@@ -176,3 +176,33 @@ def test_x4_repeat_launches_bit_identical_full_size(device, dt):
     for t in cl[1:]:
         assert torch.equal(_bits(t), _bits(cl[0]))
     assert torch.equal(_bits(cl[0]), _bits(nc[0].permute(0, 2, 3, 4, 1)))
+
+
+@pytest.mark.parametrize("n_views", (4, 8))
+@pytest.mark.parametrize("method", ("sum", "max", "softmax", "conf"))
+def test_x4_non_square_maps_and_align_corners(device, n_views, method):
+    """Non-square maps on the chunk-staged kernel (W % 4 == 0, H != W: op.py:127-130 divides
+    x by H and y by W — the reference's quirk) under both grid_sample conventions, against
+    the oracle, and bit-identical to the generic kernel."""
+    from mvn_rocm import synth
+    rng = np.random.default_rng(90 + n_views)
+    B, C, H, W = 2, 8, 56, 80
+    vb = synth.volumetric_batch(B, n_views=n_views, channels=C, heatmap=max(H, W), volume=24, seed=90 + n_views)
+    feat = rng.standard_normal((B, n_views, C, H, W)).astype(np.float32)
+    proj = vb.proj.numpy()
+    proj[:, :, 0] *= W / max(H, W)
+    proj[:, :, 1] *= H / max(H, W)
+    coords = vb.coords.numpy()
+    conf = rng.uniform(0.05, 1.0, (B, n_views, C)).astype(np.float32)
+    from mvn_rocm import _lib, op
+    F, P, X, cf = (torch.from_numpy(a).to(device) for a in (feat, proj, coords, conf))
+    for ac in (False, True):
+        a = op.unproject_heatmaps(F, P, X, method, cf, align_corners=ac)
+        with _lib.unproject_knobs(generic=True):
+            b = op.unproject_heatmaps(F, P, X, method, cf, align_corners=ac)
+        assert torch.equal(_bits(a), _bits(b)), ac
+        ref = capi.unproject(feat, proj, coords, method, conf, ac)
+        if method == "softmax":
+            assert max_rel(a.cpu().numpy(), ref) <= 1e-5
+        else:
+            assert_bits_equal(a.cpu().numpy(), ref)

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import ROOT, max_rel
+from conftest import ROOT, assert_bits_equal, max_rel
 from oracle import capi, restate_np, restate_torch
 
 METHODS = ("sum", "max", "softmax", "conf")
@@ -19,8 +19,8 @@ def test_c_oracle_unproject_small(golden, method, ac):
     out = capi.unproject(d["feat"], d["proj"], d["coords"], method, d["conf"], bool(ac))
     if method == "softmax":     # expf rounding differs from ATen's vectorised exp
         assert max_rel(out, ref) <= 1e-6
-    else:                       # bit-exact recipe
-        np.testing.assert_array_equal(out, ref)
+    else:                       # bit-exact recipe, signed zeros included
+        assert_bits_equal(out, ref)
 
 
 @pytest.mark.parametrize("method", ("sum", "softmax"))
@@ -29,7 +29,7 @@ def test_c_oracle_unproject_bf16_input(golden, method):
     out = capi.unproject(d["feat_bf16_bits"], d["proj"], d["coords"], method, None, False, feat_bf16_bits=True)
     ref = d[f"bf16in_{method}_ac0"]
     if method == "sum":
-        np.testing.assert_array_equal(out, ref)
+        assert_bits_equal(out, ref)
     else:
         assert max_rel(out, ref) <= 1e-6
 
@@ -40,7 +40,7 @@ def test_c_oracle_unproject_cfg_slice(golden, method):
     out = capi.unproject(d["feat"], d["proj"], d["coords"], method)
     ref = d[f"{method}_ac0"]
     if method == "sum":
-        np.testing.assert_array_equal(out, ref)
+        assert_bits_equal(out, ref)
     else:
         assert max_rel(out, ref) <= 1e-6
 
@@ -66,7 +66,7 @@ def test_torch_restatement_is_bit_exact(golden, method):
         out = restate_torch.unproject_heatmaps(
             torch.from_numpy(d["feat"]), torch.from_numpy(d["proj"]), torch.from_numpy(d["coords"]), method,
             torch.from_numpy(d["conf"]), align_corners=bool(ac)).numpy()
-        np.testing.assert_array_equal(out, d[f"{method}_ac{ac}"])
+        assert_bits_equal(out, d[f"{method}_ac{ac}"])
 
 
 def test_torch_restatement_rejects_unknown_aggregation(golden):

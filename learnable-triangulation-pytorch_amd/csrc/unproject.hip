@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kUnprojBlock) void unproject_regviews(
     } else if constexpr (AGG == MVN_AGG_MAX) {     // op.py:152
       r = s[0];
 #pragma unroll
-      for (int v = 1; v < kMaxRegViews; ++v) if (v < N) r = s[v] > r ? s[v] : r;
+      for (int v = 1; v < kMaxRegViews; ++v) if (v < N) r = max_takes(s[v], r) ? s[v] : r;
     } else if constexpr (AGG == MVN_AGG_CONF) {    // op.py:148: product rounded, then summed
       const float* cf = conf + size_t(b) * N * C + c;
       r = s[0] * cf[0];
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(kUnprojBlock) void unproject_anyviews(
       if constexpr (AGG == MVN_AGG_SUM) {
         r = v == 0 ? s : r + s;
       } else if constexpr (AGG == MVN_AGG_MAX) {
-        r = (v == 0 || s > r) ? s : r;
+        r = (v == 0 || max_takes(s, r)) ? s : r;
       } else if constexpr (AGG == MVN_AGG_CONF) {
         const float p = s * conf[(size_t(b) * N + v) * C + c];
         r = v == 0 ? p : r + p;

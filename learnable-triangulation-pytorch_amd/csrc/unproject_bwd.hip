@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
       }
       if constexpr (AGG == MVN_AGG_MAX) {
 #pragma unroll
-        for (int v = 1; v < NV; ++v) if (v < N && s[v] > s[arg]) arg = v;
+        for (int v = 1; v < NV; ++v) if (v < N && max_takes(s[v], s[arg])) arg = v;
       }
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
       } else if constexpr (AGG == MVN_AGG_MAX) {
         int arg = 0;
 #pragma unroll
-        for (int v = 1; v < NV; ++v) if (v < N && s[v][k] > s[arg][k]) arg = v;
+        for (int v = 1; v < NV; ++v) if (v < N && max_takes(s[v][k], s[arg][k])) arg = v;
 #pragma unroll
         for (int v = 0; v < NV; ++v) coef[v] = v == arg ? g[k] : 0.f;
       } else if constexpr (AGG == MVN_AGG_CONF) {

@@ -19,6 +19,10 @@ __device__ __forceinline__ float softmax_exp(float s, float ml) {   // ml = m * 
   return __builtin_amdgcn_exp2f(__builtin_fmaf(s, kLog2e, -ml));
 }
 
+// 'max' aggregation in torch.max(dim)'s order (ATen greater_or_nan): NaN above every number
+// (the first NaN wins), otherwise the larger value, ties to the first view.
+__device__ __forceinline__ bool max_takes(float s, float r) { return s > r || (s != s && r == r); }
+
 // Bilinear taps of one voxel in one view: 4 clamped plane offsets + 4 weights + the mask
 // of corners inside the image.  Out-of-bounds corners read the value 0 (grid_sample's
 // padding_mode='zeros': the corner VALUE is zero, so its product is +0 whatever the sign
@@ -173,7 +177,7 @@ __device__ __forceinline__ float aggregate(const float (&s)[NV], int N, const fl
   } else if constexpr (AGG == MVN_AGG_MAX) {       // op.py:152
     r = s[0];
 #pragma unroll
-    for (int v = 1; v < NV; ++v) if (v < N) r = s[v] > r ? s[v] : r;
+    for (int v = 1; v < NV; ++v) if (v < N) r = max_takes(s[v], r) ? s[v] : r;
   } else if constexpr (AGG == MVN_AGG_CONF) {      // op.py:148: product rounded, then summed
     r = s[0] * cf[0];
 #pragma unroll
@@ -261,7 +265,7 @@ __device__ __forceinline__ void gather_voxel(const TIn* __restrict__ fb, const f
         if constexpr (AGG == MVN_AGG_SUM) {
           r = v == 0 ? sv : r + sv;
         } else if constexpr (AGG == MVN_AGG_MAX) {
-          r = (v == 0 || sv > r) ? sv : r;
+          r = (v == 0 || max_takes(sv, r)) ? sv : r;
         } else if constexpr (AGG == MVN_AGG_CONF) {
           const float p = sv * cfb[size_t(v) * C + c];
           r = v == 0 ? p : r + p;
@@ -336,8 +340,8 @@ __device__ __forceinline__ f2 aggregate_pair(const f2 (&s)[NV], const f2 (&cf)[N
     f2 r = s[0];
 #pragma unroll
     for (int v = 1; v < NV; ++v) {
-      r.x = s[v].x > r.x ? s[v].x : r.x;
-      r.y = s[v].y > r.y ? s[v].y : r.y;
+      r.x = max_takes(s[v].x, r.x) ? s[v].x : r.x;
+      r.y = max_takes(s[v].y, r.y) ? s[v].y : r.y;
     }
     return r;
   } else if constexpr (AGG == MVN_AGG_CONF) {

@@ -110,7 +110,8 @@ int oracle_unproject(const void *feat, int feat_bf16, const float *P, const floa
                     for (int v = 1; v < N; ++v) r = r + s[v];
                 } else if (agg == AGG_MAX) {          /* op.py:152 */
                     r = s[0];
-                    for (int v = 1; v < N; ++v) r = s[v] > r ? s[v] : r;
+                    for (int v = 1; v < N; ++v)   /* torch.max(dim): NaN wins, ties to the first */
+                        r = (s[v] > r || (isnan(s[v]) && !isnan(r))) ? s[v] : r;
                 } else if (agg == AGG_CONF) {         /* op.py:148 */
                     const float *cf = conf + (long)b * N * C + c;
                     r = s[0] * cf[0];

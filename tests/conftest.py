@@ -44,6 +44,18 @@ def assert_bits_equal(a, b):
     assert not bad.any(), f"{int(bad.sum())} of {bad.size} elements differ in their bits (first: {a[bad][:4]} vs {b[bad][:4]})"
 
 
+def assert_parity_with_nans(out, ref, method, tol=1e-5):
+    """NaN at the same elements; elsewhere bit-equal (softmax: max_rel <= tol)."""
+    out, ref = np.asarray(out, np.float32), np.asarray(ref, np.float32)
+    nan_o, nan_r = np.isnan(out), np.isnan(ref)
+    assert (nan_o == nan_r).all(), f"NaN at {int((nan_o != nan_r).sum())} differing elements"
+    fin = ~nan_r
+    if method == "softmax":
+        assert max_rel(out[fin], ref[fin]) <= tol
+    else:
+        assert_bits_equal(out[fin], ref[fin])
+
+
 def max_rel(a, b):
     """max |a - b| / max |b| (SURVEY.md §8d parity metric)."""
     a = np.asarray(a, np.float64)

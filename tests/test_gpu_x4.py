@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import assert_bits_equal, max_rel
+from conftest import assert_bits_equal, assert_parity_with_nans, max_rel
 from oracle import capi
 
 pytestmark = pytest.mark.gpu
@@ -206,3 +206,22 @@ def test_x4_non_square_maps_and_align_corners(device, n_views, method):
             assert max_rel(a.cpu().numpy(), ref) <= 1e-5
         else:
             assert_bits_equal(a.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("n_views", (4, 8, 9))
+@pytest.mark.parametrize("method", METHODS)
+def test_nan_features_follow_the_reference(device, n_views, method):
+    """NaN feature pixels on every kernel (chunk-staged x4 at 4 / 8 views, the generic tiled
+    kernel, the simple kernel at 9 views): the outputs hold NaN exactly where the oracle
+    (pinned to torch's ops, tests/test_oracle.py) does — 'max' in torch.max(dim)'s order."""
+    from mvn_rocm import _lib, op
+    vb, conf = _batch(device, 75, heatmap=64, volume=24, channels=8, n_views=n_views)
+    feat = vb.features.numpy().copy()
+    feat.reshape(-1)[np.random.default_rng(75).choice(feat.size, 300, replace=False)] = np.nan
+    ref = capi.unproject(feat, vb.proj.numpy(), vb.coords.numpy(), method, conf.numpy())
+    assert np.isnan(ref).any()
+    F, P, X, cf = (torch.from_numpy(a).to(device) for a in (feat, vb.proj.numpy(), vb.coords.numpy(), conf.numpy()))
+    for generic in (False, True):
+        with _lib.unproject_knobs(generic=generic):
+            out = op.unproject_heatmaps(F, P, X, method, cf)
+        assert_parity_with_nans(out.cpu().numpy(), ref, method)

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import ROOT, assert_bits_equal, max_rel
+from conftest import ROOT, assert_bits_equal, assert_parity_with_nans, max_rel
 from oracle import capi, restate_np, restate_torch
 
 METHODS = ("sum", "max", "softmax", "conf")
@@ -280,3 +280,18 @@ def test_oracle_under_address_sanitizer(golden, tmp_path, method, ac, bf16):
     for b in range(B):
         for j in range(J):
             np.testing.assert_array_equal(A[b, j], capi.dlt_design(P, pts, pconf, b, j))
+
+
+@pytest.mark.parametrize("method", METHODS)
+def test_c_oracle_nan_features_follow_torch(golden, method):
+    """NaN feature pixels: the C oracle propagates them as the reference's ATen ops do —
+    through sums and the view softmax, and in 'max' with torch.max(dim)'s order (NaN above
+    every number, ties to the first view)."""
+    d = golden("unproject_small.npz")
+    feat = d["feat"].copy()
+    feat.reshape(-1)[np.random.default_rng(0).choice(feat.size, 40, replace=False)] = np.nan
+    out = capi.unproject(feat, d["proj"], d["coords"], method, d["conf"], False)
+    ref = restate_torch.unproject_heatmaps(torch.from_numpy(feat), torch.from_numpy(d["proj"]),
+                                           torch.from_numpy(d["coords"]), method, torch.from_numpy(d["conf"])).numpy()
+    assert np.isnan(ref).sum() > 50
+    assert_parity_with_nans(out, ref, method, tol=1e-6)

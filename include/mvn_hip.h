@@ -253,10 +253,13 @@ int mvn_unproject_backward(const void* feat, int feat_dtype, const float* proj, 
 
 /*
  * Deterministic variant of mvn_unproject_backward (the reference trains under
- * autograd.detect_anomaly, train.py:178; torch.use_deterministic_algorithms(True) selects
- * this in mvn_rocm): every contribution is accumulated as a 64-bit fixed-point integer with
- * 32 fraction bits (integer adds are associative), then converted to f32 — two runs are
- * bit-identical.  Range |sum| < 2^31, absolute resolution 2^-32 per contribution.
+ * autograd.detect_anomaly, train.py:178) and mvn_rocm's default backward: every contribution
+ * is scaled by a per-call power of two 2^e and accumulated as a 64-bit integer (integer adds
+ * are associative), then converted to f32 — two runs are bit-identical.  e is derived on the
+ * device from max |grad_out|, |feat| and |conf| so that no sum can overflow; the integer
+ * sums are then exact and the result is the f32 rounding of the exact sum.  Any non-finite
+ * grad_out / feat / conf value makes every output NaN.  ~4x faster than the float-atomic
+ * variant at config 2.
  *   workspace  >= mvn_unproject_backward_workspace_bytes(B, N, C, H, W) bytes, any content
  *   grad_feat / grad_conf are fully written (no zero-initialisation needed).
  */

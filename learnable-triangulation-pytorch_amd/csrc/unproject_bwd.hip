@@ -19,13 +19,15 @@
 // than scattering every tap.  Float atomics make the result order-nondeterministic in the
 // last bits (documented in DESIGN.md).
 //
-// Deterministic mode (DET; mvn_unproject_backward_deterministic, selected by the Python layer
-// under torch.use_deterministic_algorithms(True)): every contribution — the same f32 product
-// as above — is quantised to a 64-bit fixed-point integer with 32 fraction bits, and both
-// the LDS and the global accumulation are integer adds (ds_add_u64 / global_atomic_add_x2),
-// which are associative: the sums do not depend on the order the waves and blocks arrive
-// in, so two runs are bit-identical.  A last kernel converts the integers back to f32.
-// Contract of the mode: |gradient sums| < 2^31, absolute resolution 2^-32 per contribution.
+// Fixed-point mode (DET; mvn_unproject_backward_deterministic — the Python layer's default):
+// every contribution — the same f32 product as above — is scaled by a per-call power of two
+// 2^e and rounded to a 64-bit integer; the LDS and the global accumulation are integer adds
+// (ds_add_u64 / global_atomic_add_x2), which are associative, so the sums do not depend on
+// the order the waves and blocks arrive in and two runs are bit-identical.  e comes from
+// the inputs' magnitudes on the device (absmax_bits, fix_scale: no host sync) so that no sum
+// can overflow; at that scale the contributions convert exactly, the integer sums are exact
+// and the last kernel's conversion gives the f32 rounding of the exact sum (a float-atomic
+// sum rounds at every add).  A non-finite input makes every gradient NaN.
 #include <algorithm>
 
 #include "unproject_common.hpp"
@@ -43,17 +45,34 @@ constexpr int TX = 4, TY = 8, TZ = 8;        // one voxel per thread
 
 template <typename T> __device__ __forceinline__ float ldf(const T* p, size_t i) { return to_f32(p[i]); }
 
-// deterministic mode: f32 contribution -> 32.32 fixed point (round to nearest; clamped far
-// outside the mode's range so the conversion is defined)
-constexpr float kFix = 4294967296.f;           // 2^32
-__device__ __forceinline__ unsigned long long to_fix(float x) {
-  const float y = fminf(fmaxf(x * kFix, -0x1p62f), 0x1p62f);
+// Fixed-point mode (DET): an f32 contribution x becomes round(x * 2^e) in a 64-bit integer.
+// e is chosen per call on the device (fix_scale) from the inputs' magnitudes so that no sum
+// can leave +-2^62: |every accumulated sum| <= nvox * max|g| * max(1, max|conf|) *
+// (1 + 2 max|feat|) (bilinear weights of a voxel-view sum to <= 1; |d agg / d s| <= 1 + 2
+// max|s| for softmax, conf for conf*).  Typical contributions are then >= 2^24 units, so
+// the scaling and the integer conversion are exact and the integer sums are exact: the
+// result is the f32 rounding of the exact sum, in any arrival order.  (Clamp: guard only.)
+__device__ __forceinline__ unsigned long long to_fix(float x, float scale) {
+  const float y = fminf(fmaxf(x * scale, -0x1p62f), 0x1p62f);
   return static_cast<unsigned long long>(__float2ll_rn(y));
 }
+// per-call header at the start of the fixed-point workspace
+struct FixHeader {
+  unsigned gbits, fbits, cbits, pad;   // max |grad_out|, |feat|, |conf| as f32 bits (NaN above inf)
+  float scale;                         // 2^e
+  int valid;                           // 0: a non-finite input; the gradients are NaN
+  double inv;                          // 2^-e
+};
+// header, then per-block partial maxima of |grad_out|, |feat|, |conf| (kMaxParts each): the
+// maxima are reduced in two levels without atomics (thousands of same-address atomics
+// serialise at the memory side)
+constexpr int kMaxParts = 1024;
+constexpr size_t kFixPartsOffset = 256;
+constexpr size_t kFixHeaderBytes = kFixPartsOffset + 3 * kMaxParts * sizeof(unsigned);
 // float accumulate (default) or fixed-point accumulate (DET) into a global element
 template <bool DET>
-__device__ __forceinline__ void global_add(float* f, unsigned long long* q, size_t i, float x) {
-  if constexpr (DET) atomicAdd(q + i, to_fix(x));
+__device__ __forceinline__ void global_add(float* f, unsigned long long* q, size_t i, float x, float scale) {
+  if constexpr (DET) atomicAdd(q + i, to_fix(x, scale));
   else atomicAdd(f + i, x);
 }
 
@@ -62,16 +81,18 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ conf, const TG* __restrict__ gout, float* __restrict__ gfeat,
     float* __restrict__ gconf, unsigned long long* __restrict__ qfeat, unsigned long long* __restrict__ qconf,
-    int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners) {
+    const float* __restrict__ fixscale, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners) {
   constexpr bool kNeedSamples = AGG == MVN_AGG_SOFTMAX || AGG == MVN_AGG_MAX || AGG == MVN_AGG_CONF;
   __shared__ float4 fstage[kSlots];          // forward features (channels-last)
   __shared__ float4 gacc[DET ? 1 : kSlots];  // gradient accumulator (channels-last)
-  __shared__ unsigned long long gq[DET ? kSlots * G : 1];   // the same in 32.32 fixed point (DET)
+  __shared__ unsigned long long gq[DET ? kSlots * G : 1];   // the same in fixed point (DET)
   __shared__ int red[kWaves][NV][4];
   __shared__ int region[NV][5];              // xs, ys, bw, pitch, base
   __shared__ float gconf_acc[NV][G];
   __shared__ unsigned long long gconf_q[DET ? NV : 1][G];
   __shared__ int info[2];                    // total slots (or -1: direct global path)
+  float fsc = 0.f;                           // 2^e of this call (DET)
+  if constexpr (DET) fsc = *fixscale;
 
   const int nTx = (Vx + TX - 1) / TX, nTy = (Vy + TY - 1) / TY, nTz = (Vz + TZ - 1) / TZ;
   int L = xcd_remap(blockIdx.x, B * nTx * nTy * nTz);
@@ -179,13 +200,13 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
         else coef[v] = g * (softmax_exp(s[v], m * kLog2e) * __builtin_amdgcn_rcpf(den)) * (1.f + s[v] - out);
         if (coef[v] != 0.f) {
           const size_t pl = fbo + (size_t(v) * C + c) * HW;
-          if (tp[v].w0 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o0, coef[v] * tp[v].w0);
-          if (tp[v].w1 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o1, coef[v] * tp[v].w1);
-          if (tp[v].w2 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o2, coef[v] * tp[v].w2);
-          if (tp[v].w3 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o3, coef[v] * tp[v].w3);
+          if (tp[v].w0 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o0, coef[v] * tp[v].w0, fsc);
+          if (tp[v].w1 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o1, coef[v] * tp[v].w1, fsc);
+          if (tp[v].w2 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o2, coef[v] * tp[v].w2, fsc);
+          if (tp[v].w3 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o3, coef[v] * tp[v].w3, fsc);
         }
         if constexpr (AGG == MVN_AGG_CONF)
-          if (gconf && v < N && g * s[v] != 0.f) global_add<DET>(gconf, qconf, (size_t(b) * N + v) * C + c, g * s[v]);
+          if (gconf && v < N && g * s[v] != 0.f) global_add<DET>(gconf, qconf, (size_t(b) * N + v) * C + c, g * s[v], fsc);
       }
     }
     return;
@@ -291,10 +312,10 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
         if constexpr (DET) {
           unsigned long long* q0 = &gq[slot[v] * G + k];
           unsigned long long* q1 = &gq[(slot[v] + rpitch[v]) * G + k];
-          atomicAdd(q0, to_fix(coef[v] * w[v][0]));
-          atomicAdd(q0 + G, to_fix(coef[v] * w[v][1]));
-          atomicAdd(q1, to_fix(coef[v] * w[v][2]));
-          atomicAdd(q1 + G, to_fix(coef[v] * w[v][3]));
+          atomicAdd(q0, to_fix(coef[v] * w[v][0], fsc));
+          atomicAdd(q0 + G, to_fix(coef[v] * w[v][1], fsc));
+          atomicAdd(q1, to_fix(coef[v] * w[v][2], fsc));
+          atomicAdd(q1 + G, to_fix(coef[v] * w[v][3], fsc));
         } else {
           float* base0 = reinterpret_cast<float*>(&gacc[slot[v]]) + k;
           float* base1 = reinterpret_cast<float*>(&gacc[slot[v] + rpitch[v]]) + k;
@@ -313,7 +334,7 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
             if (lane == 0 && part != 0.f) {
-              if constexpr (DET) atomicAdd(&gconf_q[v][k], to_fix(part));
+              if constexpr (DET) atomicAdd(&gconf_q[v][k], to_fix(part, fsc));
               else atomicAdd(&gconf_acc[v][k], part);
             }
           }
@@ -364,24 +385,74 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
   }
 }
 
-// fixed-point sums (DET) -> f32 gradients
-__global__ void fix_to_f32(const unsigned long long* __restrict__ q, float* __restrict__ out, size_t n) {
+// max |x| of a tensor as f32 bits (|x| >= 0 orders like its bits; NaN's bits sort above inf):
+// one partial per block into part[blockIdx.x] (gridDim.x <= kMaxParts)
+template <typename T>
+__global__ __launch_bounds__(256) void absmax_bits(const T* __restrict__ x, size_t n, unsigned* __restrict__ part) {
+  __shared__ unsigned wmax[256 / kWave];
+  unsigned m = 0;
   for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-    out[i] = float(double(static_cast<long long>(q[i])) * 0x1p-32);
+    m = max(m, __float_as_uint(fabsf(to_f32(x[i]))));
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) m = max(m, unsigned(__shfl_xor(int(m), o, kWave)));
+  if ((threadIdx.x & (kWave - 1)) == 0) wmax[threadIdx.x / kWave] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned b = 0;
+#pragma unroll
+    for (int w = 0; w < 256 / kWave; ++w) b = max(b, wmax[w]);
+    part[blockIdx.x] = b;
+  }
+}
+// the call's fixed-point exponent from the partial maxima (one block of 256 threads)
+__global__ __launch_bounds__(256) void fix_scale(FixHeader* __restrict__ h, const unsigned* __restrict__ parts,
+                                                 double nvox) {
+  __shared__ unsigned red[3][256 / kWave];
+  unsigned m[3] = {0u, 0u, 0u};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    for (int i = threadIdx.x; i < kMaxParts; i += 256) m[k] = max(m[k], parts[k * kMaxParts + i]);
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) m[k] = max(m[k], unsigned(__shfl_xor(int(m[k]), o, kWave)));
+    if ((threadIdx.x & (kWave - 1)) == 0) red[k][threadIdx.x / kWave] = m[k];
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  unsigned gb = 0, fb = 0, cb = 0;
+#pragma unroll
+  for (int w = 0; w < 256 / kWave; ++w) { gb = max(gb, red[0][w]); fb = max(fb, red[1][w]); cb = max(cb, red[2][w]); }
+  const bool finite = gb < 0x7f800000u && fb < 0x7f800000u && cb < 0x7f800000u;
+  const double g = __uint_as_float(gb), f = __uint_as_float(fb), c = __uint_as_float(cb);
+  const double bound = nvox * g * fmax(1.0, c) * (1.0 + 2.0 * f);
+  int e = 62;
+  if (finite && bound > 0.0) e = int(floor(62.0 - log2(bound))) - 1;
+  e = min(max(e, -120), 120);
+  h->gbits = gb; h->fbits = fb; h->cbits = cb;
+  h->scale = ldexpf(1.f, e);
+  h->inv = ldexp(1.0, -e);
+  h->valid = finite ? 1 : 0;
+}
+// fixed-point sums (DET) -> f32 gradients
+__global__ void fix_to_f32(const unsigned long long* __restrict__ q, float* __restrict__ out, size_t n,
+                           const FixHeader* __restrict__ h) {
+  const double inv = h->inv;
+  const bool valid = h->valid != 0;
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+    out[i] = valid ? float(double(static_cast<long long>(q[i])) * inv) : __builtin_nanf("");
 }
 
 template <int AGG, typename TIn, typename TG, bool DET>
 int launch_bwd(const void* feat, const float* P, const float* coords, const float* conf, const void* gout, float* gfeat,
-               float* gconf, unsigned long long* qfeat, unsigned long long* qconf, int B, int N, int C, int H, int W,
-               int Vx, int Vy, int Vz, int ac, hipStream_t s) {
+               float* gconf, unsigned long long* qfeat, unsigned long long* qconf, const float* fixs, int B, int N,
+               int C, int H, int W, int Vx, int Vy, int Vz, int ac, hipStream_t s) {
   const long long nb = (long long)B * ((Vx + TX - 1) / TX) * ((Vy + TY - 1) / TY) * ((Vz + TZ - 1) / TZ);
   if (nb > INT_MAX) return MVN_ERR_SHAPE;
   if (N <= 4)
     unproject_bwd_tiled<AGG, TIn, TG, 4, DET><<<int(nb), kThreads, 0, s>>>(static_cast<const TIn*>(feat), P, coords,
-        conf, static_cast<const TG*>(gout), gfeat, gconf, qfeat, qconf, B, N, C, H, W, Vx, Vy, Vz, ac);
+        conf, static_cast<const TG*>(gout), gfeat, gconf, qfeat, qconf, fixs, B, N, C, H, W, Vx, Vy, Vz, ac);
   else if (N <= 8)
     unproject_bwd_tiled<AGG, TIn, TG, 8, DET><<<int(nb), kThreads, 0, s>>>(static_cast<const TIn*>(feat), P, coords,
-        conf, static_cast<const TG*>(gout), gfeat, gconf, qfeat, qconf, B, N, C, H, W, Vx, Vy, Vz, ac);
+        conf, static_cast<const TG*>(gout), gfeat, gconf, qfeat, qconf, fixs, B, N, C, H, W, Vx, Vy, Vz, ac);
   else
     return MVN_ERR_SHAPE;
   return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
@@ -389,20 +460,20 @@ int launch_bwd(const void* feat, const float* P, const float* coords, const floa
 
 template <typename TIn, typename TG, bool DET>
 int dispatch_bwd(int agg, const void* feat, const float* P, const float* coords, const float* conf, const void* gout,
-                 float* gfeat, float* gconf, unsigned long long* qfeat, unsigned long long* qconf, int B, int N, int C,
-                 int H, int W, int Vx, int Vy, int Vz, int ac, hipStream_t s) {
+                 float* gfeat, float* gconf, unsigned long long* qfeat, unsigned long long* qconf, const float* fixs,
+                 int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int ac, hipStream_t s) {
   switch (agg) {
     case MVN_AGG_SUM:
-      return launch_bwd<MVN_AGG_SUM, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, B, N, C, H,
+      return launch_bwd<MVN_AGG_SUM, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, fixs, B, N, C, H,
                                                    W, Vx, Vy, Vz, ac, s);
     case MVN_AGG_MAX:
-      return launch_bwd<MVN_AGG_MAX, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, B, N, C, H,
+      return launch_bwd<MVN_AGG_MAX, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, fixs, B, N, C, H,
                                                    W, Vx, Vy, Vz, ac, s);
     case MVN_AGG_SOFTMAX:
-      return launch_bwd<MVN_AGG_SOFTMAX, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, B, N,
+      return launch_bwd<MVN_AGG_SOFTMAX, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, fixs, B, N,
                                                        C, H, W, Vx, Vy, Vz, ac, s);
     case MVN_AGG_CONF:
-      return launch_bwd<MVN_AGG_CONF, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, B, N, C,
+      return launch_bwd<MVN_AGG_CONF, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, fixs, B, N, C,
                                                     H, W, Vx, Vy, Vz, ac, s);
   }
   return MVN_ERR_ARG;
@@ -411,20 +482,20 @@ int dispatch_bwd(int agg, const void* feat, const float* P, const float* coords,
 template <bool DET>
 int backward_entry(const void* feat, int feat_dtype, const float* proj, const float* coords, const float* conf,
                    const void* grad_out, int grad_out_dtype, float* grad_feat, float* grad_conf,
-                   unsigned long long* qfeat, unsigned long long* qconf, int B, int N, int C, int H, int W, int Vx,
-                   int Vy, int Vz, int agg, int align_corners, hipStream_t s) {
+                   unsigned long long* qfeat, unsigned long long* qconf, const float* fixs, int B, int N, int C, int H,
+                   int W, int Vx, int Vy, int Vz, int agg, int align_corners, hipStream_t s) {
   const bool f16 = feat_dtype == MVN_DTYPE_BF16, g16 = grad_out_dtype == MVN_DTYPE_BF16;
   if ((feat_dtype != MVN_DTYPE_F32 && !f16) || (grad_out_dtype != MVN_DTYPE_F32 && !g16)) return MVN_ERR_DTYPE;
   if (!f16 && !g16)
-    return dispatch_bwd<float, float, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat, qconf,
+    return dispatch_bwd<float, float, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat, qconf, fixs,
                                            B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
   if (f16 && g16)
     return dispatch_bwd<uint16_t, uint16_t, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat,
-                                                 qconf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+                                                 qconf, fixs, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
   if (f16)
     return dispatch_bwd<uint16_t, float, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat,
-                                              qconf, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
-  return dispatch_bwd<float, uint16_t, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat, qconf,
+                                              qconf, fixs, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+  return dispatch_bwd<float, uint16_t, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat, qconf, fixs,
                                             B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
 }
 
@@ -454,13 +525,13 @@ extern "C" int mvn_unproject_backward(const void* feat, int feat_dtype, const fl
                                align_corners);
   if (e != MVN_OK) return e;
   return backward_entry<false>(feat, feat_dtype, proj, coords, conf, grad_out, grad_out_dtype, grad_feat, grad_conf,
-                               nullptr, nullptr, B, N, C, H, W, Vx, Vy, Vz, agg, align_corners,
+                               nullptr, nullptr, nullptr, B, N, C, H, W, Vx, Vy, Vz, agg, align_corners,
                                static_cast<hipStream_t>(stream));
 }
 
 extern "C" size_t mvn_unproject_backward_workspace_bytes(int B, int N, int C, int H, int W) {
   if (B <= 0 || N <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
-  return (size_t(B) * N * C * size_t(H) * W + size_t(B) * N * C) * sizeof(unsigned long long);
+  return mvn::unproj::kFixHeaderBytes + (size_t(B) * N * C * size_t(H) * W + size_t(B) * N * C) * sizeof(unsigned long long);
 }
 
 extern "C" int mvn_unproject_backward_deterministic(const void* feat, int feat_dtype, const float* proj,
@@ -477,16 +548,31 @@ extern "C" int mvn_unproject_backward_deterministic(const void* feat, int feat_d
   const size_t nfeat = size_t(B) * N * C * size_t(H) * W, nconf = size_t(B) * N * C;
   if (!workspace || workspace_bytes < mvn_unproject_backward_workspace_bytes(B, N, C, H, W)) return MVN_ERR_WORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  auto* qfeat = static_cast<unsigned long long*>(workspace);
+  auto* hdr = static_cast<FixHeader*>(workspace);
+  auto* qfeat = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + kFixHeaderBytes);
   auto* qconf = qfeat + nfeat;
-  if (hipMemsetAsync(workspace, 0, (nfeat + nconf) * sizeof(unsigned long long), s) != hipSuccess)
+  if (hipMemsetAsync(workspace, 0, kFixHeaderBytes + (nfeat + nconf) * sizeof(unsigned long long), s) != hipSuccess)
     return MVN_ERR_LAUNCH;
+  // the call's fixed-point scale from max |grad_out|, |feat|, |conf| (device-side: no sync)
+  auto* parts = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + kFixPartsOffset);
+  const size_t ngrad = size_t(B) * C * size_t(Vx) * Vy * Vz;
+  auto nblk_of = [](size_t n) { return int(std::min<size_t>((n + 255) / 256, kMaxParts)); };
+  if (grad_out_dtype == MVN_DTYPE_BF16)
+    absmax_bits<<<nblk_of(ngrad), 256, 0, s>>>(static_cast<const uint16_t*>(grad_out), ngrad, parts);
+  else
+    absmax_bits<<<nblk_of(ngrad), 256, 0, s>>>(static_cast<const float*>(grad_out), ngrad, parts);
+  if (feat_dtype == MVN_DTYPE_BF16)
+    absmax_bits<<<nblk_of(nfeat), 256, 0, s>>>(static_cast<const uint16_t*>(feat), nfeat, parts + kMaxParts);
+  else
+    absmax_bits<<<nblk_of(nfeat), 256, 0, s>>>(static_cast<const float*>(feat), nfeat, parts + kMaxParts);
+  if (agg == MVN_AGG_CONF) absmax_bits<<<nblk_of(nconf), 256, 0, s>>>(conf, nconf, parts + 2 * kMaxParts);
+  fix_scale<<<1, 256, 0, s>>>(hdr, parts, double(Vx) * Vy * Vz);
   const int r = backward_entry<true>(feat, feat_dtype, proj, coords, conf, grad_out, grad_out_dtype, grad_feat,
-                                     grad_conf, qfeat, grad_conf ? qconf : nullptr, B, N, C, H, W, Vx, Vy, Vz, agg,
-                                     align_corners, s);
+                                     grad_conf, qfeat, grad_conf ? qconf : nullptr, &hdr->scale, B, N, C, H, W, Vx,
+                                     Vy, Vz, agg, align_corners, s);
   if (r != MVN_OK) return r;
-  const int nblk = int(std::min<size_t>((nfeat + 255) / 256, 65536));
-  fix_to_f32<<<nblk, 256, 0, s>>>(qfeat, grad_feat, nfeat);
-  if (grad_conf) fix_to_f32<<<int(std::min<size_t>((nconf + 255) / 256, 65536)), 256, 0, s>>>(qconf, grad_conf, nconf);
+  auto cvt_blocks = [](size_t n) { return int(std::min<size_t>((n + 255) / 256, 65536)); };
+  fix_to_f32<<<cvt_blocks(nfeat), 256, 0, s>>>(qfeat, grad_feat, nfeat, hdr);
+  if (grad_conf) fix_to_f32<<<cvt_blocks(nconf), 256, 0, s>>>(qconf, grad_conf, nconf, hdr);
   return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
 }

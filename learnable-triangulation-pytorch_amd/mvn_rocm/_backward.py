@@ -16,6 +16,13 @@ from . import _lib
 from ._ops import _DTYPE_CODE, _op, _ptr, _require_gpu, _stream, call
 
 
+# Accumulation of the unprojection backward: "fixed" (default) — per-call-scaled 64-bit
+# fixed point (mvn_unproject_backward_deterministic): bit-identical across runs, the f32
+# rounding of the exact sums, and ~4x faster than "float_atomic" (mvn_unproject_backward,
+# order-dependent f32 atomics; kept for A/B and for callers that want no workspace).
+UNPROJECT_BACKWARD = "fixed"
+
+
 @_op("unproject_backward")
 def unproject_bwd(feat: Tensor, proj: Tensor, coords: Tensor, conf: Optional[Tensor], grad_out: Tensor, agg: int,
                   align_corners: bool, want_conf: bool) -> List[Tensor]:
@@ -33,9 +40,9 @@ def unproject_bwd(feat: Tensor, proj: Tensor, coords: Tensor, conf: Optional[Ten
         # gradients; the forward launched nothing either (ops return the empty volume)
         return [gfeat.to(feat.dtype), gconf]
     lib = _lib.load()
-    if torch.are_deterministic_algorithms_enabled():
-        # torch.use_deterministic_algorithms(True): fixed-point accumulation, bit-identical
-        # across runs (mvn_unproject_backward_deterministic)
+    if UNPROJECT_BACKWARD == "fixed" or torch.are_deterministic_algorithms_enabled():
+        # fixed-point accumulation, bit-identical across runs (always under
+        # torch.use_deterministic_algorithms(True))
         ws = torch.empty(lib.mvn_unproject_backward_workspace_bytes(B, N, C, H, W), dtype=torch.uint8,
                          device=feat.device)
         code = lib.mvn_unproject_backward_deterministic(

@@ -136,11 +136,12 @@ def test_unproject_v2v_front_argument_validation(lib):
 
 def test_deterministic_backward_argument_checks(lib):
     """mvn_unproject_backward_deterministic validates before any HIP call: the workspace
-    (64-bit fixed-point sums: one per feature element and per confidence) must be present and
-    large enough (MVN_ERR_WORKSPACE), shapes and enums as mvn_unproject_backward."""
+    (a header for the per-call scale and its partial maxima, then 64-bit fixed-point sums: one per feature
+    element and per confidence) must be present and large enough (MVN_ERR_WORKSPACE), shapes
+    and enums as mvn_unproject_backward."""
     B, N, C, H, W = 2, 4, 8, 24, 24
     need = lib.mvn_unproject_backward_workspace_bytes(B, N, C, H, W)
-    assert need == (B * N * C * H * W + B * N * C) * 8
+    assert need == 256 + 3 * 1024 * 4 + (B * N * C * H * W + B * N * C) * 8
     assert lib.mvn_unproject_backward_workspace_bytes(0, N, C, H, W) == 0
 
     def call(ws=1, ws_bytes=need, agg=0, B_=B, N_=N):

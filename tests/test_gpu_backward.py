@@ -112,45 +112,73 @@ def test_softargmax2d_backward_matches_reference_autograd(golden, device, softma
 
 
 @pytest.mark.parametrize("method", ("sum", "softmax", "conf"))
-def test_unproject_backward_deterministic_mode(golden, device, method):
-    """Under torch.use_deterministic_algorithms(True) the unprojection backward accumulates
-    in 32.32 fixed point (mvn_unproject_backward_deterministic): two runs are bit-identical —
-    the golden case, a config-sized scatter with thousands of colliding taps per pixel, and the
-    LDS-overflow (global scatter) path — and the gradients stay within 1e-5 of the reference's
-    autograd.  (The reference's own training loop runs under autograd.detect_anomaly,
-    train.py:178.)"""
-    from mvn_rocm import op, synth
+def test_unproject_backward_fixed_point_mode(golden, device, method):
+    """The default unprojection backward accumulates in per-call-scaled 64-bit fixed point
+    (mvn_unproject_backward_deterministic): two runs are bit-identical — the golden case, a
+    config-sized scatter with thousands of colliding taps per pixel, and the LDS-overflow
+    (global scatter) path — the gradients stay within 1e-5 of the reference's autograd and
+    within 1e-6 of the float-atomic path, also under torch.use_deterministic_algorithms(True)
+    (the reference's own training loop runs under autograd.detect_anomaly, train.py:178)."""
+    from mvn_rocm import _backward, op, synth
     d = golden("unproject_small.npz")
     key = f"{method}_ac0"
-    prev = torch.are_deterministic_algorithms_enabled()
-    torch.use_deterministic_algorithms(True)
-    try:
-        def run(feat_np, P, coords, conf_np, gout):
+
+    def run(feat_np, P, coords, conf_np, gout, mode="fixed"):
+        prev = _backward.UNPROJECT_BACKWARD
+        _backward.UNPROJECT_BACKWARD = mode
+        try:
             feat = _t(feat_np, device).requires_grad_(True)
             conf = _t(conf_np, device).requires_grad_(True) if conf_np is not None else None
             out = op.unproject_heatmaps(feat, P, coords, method, conf)
             out.backward(gout)
             return feat.grad.clone(), (conf.grad.clone() if conf is not None else None)
+        finally:
+            _backward.UNPROJECT_BACKWARD = prev
 
-        P, coords = _t(d["proj"], device), _t(d["coords"], device)
-        conf_np = d["conf"] if method == "conf" else None
-        g1, c1 = run(d["feat"], P, coords, conf_np, _t(d[f"grad_out_{key}"], device))
-        g2, c2 = run(d["feat"], P, coords, conf_np, _t(d[f"grad_out_{key}"], device))
-        assert torch.equal(g1.view(torch.int32), g2.view(torch.int32))
-        assert max_rel(g1.cpu().numpy(), d[f"grad_feat_{key}"]) <= 1e-5
-        if method == "conf":
-            assert torch.equal(c1.view(torch.int32), c2.view(torch.int32))
-            assert max_rel(c1.cpu().numpy(), d[f"grad_conf_{key}"]) <= 1e-5
-        for heatmap, volume in ((96, 32), (96, 16)):          # (96, 16): the LDS-overflow global path
-            vb = synth.volumetric_batch(2, n_views=4, channels=8, heatmap=heatmap, volume=volume, seed=9)
-            cf = np.random.default_rng(9).uniform(0.1, 1, (2, 4, 8)).astype(np.float32) if method == "conf" else None
-            gout = torch.randn((2, 8, volume, volume, volume), generator=torch.Generator().manual_seed(2)).to(device)
-            a = run(vb.features.numpy(), vb.proj.to(device), vb.coords.to(device), cf, gout)[0]
-            b = run(vb.features.numpy(), vb.proj.to(device), vb.coords.to(device), cf, gout)[0]
-            assert torch.equal(a.view(torch.int32), b.view(torch.int32))
-            torch.use_deterministic_algorithms(False)
-            f = run(vb.features.numpy(), vb.proj.to(device), vb.coords.to(device), cf, gout)[0]
-            torch.use_deterministic_algorithms(True)
-            assert max_rel(a.cpu().numpy(), f.cpu().numpy()) <= 1e-6
+    P, coords = _t(d["proj"], device), _t(d["coords"], device)
+    conf_np = d["conf"] if method == "conf" else None
+    g1, c1 = run(d["feat"], P, coords, conf_np, _t(d[f"grad_out_{key}"], device))
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True)
+    try:
+        g2, c2 = run(d["feat"], P, coords, conf_np, _t(d[f"grad_out_{key}"], device), mode="float_atomic")
     finally:
         torch.use_deterministic_algorithms(prev)
+    assert torch.equal(g1.view(torch.int32), g2.view(torch.int32))     # the flag forces the fixed path
+    assert max_rel(g1.cpu().numpy(), d[f"grad_feat_{key}"]) <= 1e-5
+    if method == "conf":
+        assert torch.equal(c1.view(torch.int32), c2.view(torch.int32))
+        assert max_rel(c1.cpu().numpy(), d[f"grad_conf_{key}"]) <= 1e-5
+    for heatmap, volume in ((96, 32), (96, 16)):          # (96, 16): the LDS-overflow global path
+        vb = synth.volumetric_batch(2, n_views=4, channels=8, heatmap=heatmap, volume=volume, seed=9)
+        cf = np.random.default_rng(9).uniform(0.1, 1, (2, 4, 8)).astype(np.float32) if method == "conf" else None
+        gout = torch.randn((2, 8, volume, volume, volume), generator=torch.Generator().manual_seed(2)).to(device)
+        a = run(vb.features.numpy(), vb.proj.to(device), vb.coords.to(device), cf, gout)[0]
+        b = run(vb.features.numpy(), vb.proj.to(device), vb.coords.to(device), cf, gout)[0]
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+        f = run(vb.features.numpy(), vb.proj.to(device), vb.coords.to(device), cf, gout, mode="float_atomic")[0]
+        assert max_rel(a.cpu().numpy(), f.cpu().numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("scale", (1e-30, 1e-8, 1e8, 1e30))
+def test_unproject_backward_fixed_point_scale_follows_the_data(device, scale):
+    """The fixed-point exponent is chosen per call from the inputs' magnitudes: gradients
+    scaled by 1e-30 ... 1e30 come out as the same relative values (no underflow to zero, no
+    overflow) — a fixed 32.32 format would lose the 1e-8 case entirely and overflow at 1e30.
+    A non-finite upstream gradient makes every output NaN (the mode's contract)."""
+    from mvn_rocm import op, synth
+    vb = synth.volumetric_batch(2, n_views=4, channels=8, heatmap=96, volume=24, seed=12)
+    gout = torch.randn((2, 8, 24, 24, 24), generator=torch.Generator().manual_seed(3)).to(device)
+
+    def grad(g):
+        f = vb.features.to(device).requires_grad_(True)
+        op.unproject_heatmaps(f, vb.proj.to(device), vb.coords.to(device), "softmax").backward(g)
+        return f.grad.cpu().numpy().astype(np.float64)
+
+    base = grad(gout)
+    scaled = grad(gout * scale) / scale
+    assert np.abs(base).max() > 0
+    assert max_rel(scaled, base) <= 1e-6
+    g_nan = gout.clone()
+    g_nan[0, 0, 0, 0, 0] = float("nan")
+    assert np.isnan(grad(g_nan)).all()

@@ -305,6 +305,16 @@ int mvn_dlt_backward(const float* proj, const float* pts, const float* conf, con
 int mvn_debug_set_unproject(int lds_slots, int kernel);
 
 /*
+ * Debug build only (make -C learnable-triangulation-pytorch_amd debug -> libmvn_hip_debug.so,
+ * -DMVN_DEVICE_ASSERTS): device-side index / layout assertions count their failures instead of
+ * trapping.  Reads and clears the counters of every kernel file: *enabled = 1 in the debug
+ * build (0 in the release build, whose kernels carry no checks), *count = failures since the
+ * last call, *first_line = source line of the first (0 when none).  Synchronise the device
+ * first.  Returns MVN_OK, MVN_ERR_ARG for a null pointer, MVN_ERR_LAUNCH if a copy fails.
+ */
+int mvn_debug_device_asserts(int* enabled, unsigned* count, unsigned* first_line);
+
+/*
  * Diagnostics: workgroups of the four-view unprojection kernel resident per CU (its LDS and
  * register budget; the persistent grid is this x the CU count), for f32 (bf16_maps = 0) or
  * bf16 (1) feature maps.  Needs a device; returns a count >= 1.

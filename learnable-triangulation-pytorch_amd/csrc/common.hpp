@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "mvn_hip.h"
 
 namespace mvn {
@@ -73,6 +75,44 @@ __device__ __forceinline__ void cuboid_coord(const float* __restrict__ cub, int 
 }
 
 inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
+
+// ---- device-side assertions (debug build: make debug -> libmvn_hip_debug.so) ----------------
+// SURVEY.md §5 'race detection / sanitizers'.  MVN_DASSERT(cond) checks an index or layout
+// invariant inside a kernel.  A failure does not trap (a GPU fault takes the whole device down):
+// it counts into a per-translation-unit device word and keeps the first failing line; the host
+// reads and clears every unit's words through mvn_debug_device_asserts() (tests/conftest.py
+// checks it after every GPU test when the debug library is loaded).  Release builds compile the
+// checks away.
+using DassertReader = int (*)(unsigned* count, unsigned* line);
+std::vector<DassertReader>& dassert_registry();      // defined in unproject.hip
+#ifdef MVN_DEVICE_ASSERTS
+namespace {
+__device__ unsigned g_dassert[2];                    // failures, first failing line (this unit)
+int dassert_read_clear(unsigned* count, unsigned* line) {
+  unsigned v[2] = {0u, 0u};
+  if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_dassert), sizeof(v)) != hipSuccess) return -1;
+  const unsigned zero[2] = {0u, 0u};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_dassert), zero, sizeof(zero)) != hipSuccess) return -1;
+  *count = v[0];
+  *line = v[1];
+  return 0;
+}
+const bool g_dassert_registered = (dassert_registry().push_back(&dassert_read_clear), true);
+}  // namespace
+#define MVN_DASSERT(cond)                                                         \
+  do {                                                                            \
+    if (!(cond)) {                                                                \
+      if (__hip_atomic_fetch_add(&::mvn::g_dassert[0], 1u, __ATOMIC_RELAXED,      \
+                                 __HIP_MEMORY_SCOPE_AGENT) == 0u)                 \
+        __hip_atomic_store(&::mvn::g_dassert[1], unsigned(__LINE__), __ATOMIC_RELAXED, \
+                           __HIP_MEMORY_SCOPE_AGENT);                             \
+    }                                                                             \
+  } while (0)
+#else
+#define MVN_DASSERT(cond) \
+  do {                    \
+  } while (0)
+#endif
 
 // Test-only knobs of the unprojection dispatch (mvn_debug_set_unproject, unproject.hip):
 // process-wide atomics set by tests to force the multi-pass / global-gather / simple

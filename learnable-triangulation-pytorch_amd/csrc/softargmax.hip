@@ -242,6 +242,7 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     float q[kPartial];
     reduce_values(x, q);
     if (lane == kWave - 1) {
+      MVN_DASSERT(j < J && chunk < nchunk);
       float* o = part + ((size_t(b) * J + j) * nchunk + chunk) * kPartial;
 #pragma unroll
       for (int k = 0; k < kPartial; ++k) o[k] = q[k];
@@ -278,6 +279,7 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     float acc[kPartial] = {0.f, 0.f, 0.f, 0.f, 0.f};
     auto flush = [&](int jbase, int n) __attribute__((always_inline)) {
       if (lane < n) {
+        MVN_DASSERT(jbase + lane < J && chunk < nchunk);
         float* o = part + ((size_t(b) * J + jbase + lane) * nchunk + chunk) * kPartial;
 #pragma unroll
         for (int k = 0; k < kPartial; ++k) o[k] = acc[k];

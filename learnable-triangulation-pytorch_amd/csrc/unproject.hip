@@ -227,6 +227,31 @@ extern "C" int mvn_debug_unproject_occupancy(int bf16_maps) {
   return mvn::unproj::x4_blocks_per_cu(bf16_maps ? 1 : 0);
 }
 
+namespace mvn {
+std::vector<DassertReader>& dassert_registry() {
+  static std::vector<DassertReader> r;
+  return r;
+}
+}  // namespace mvn
+
+extern "C" int mvn_debug_device_asserts(int* enabled, unsigned* count, unsigned* first_line) {
+  if (!enabled || !count || !first_line) return MVN_ERR_ARG;
+#ifdef MVN_DEVICE_ASSERTS
+  *enabled = 1;
+#else
+  *enabled = 0;
+#endif
+  *count = 0;
+  *first_line = 0;
+  for (auto rd : mvn::dassert_registry()) {
+    unsigned c = 0, l = 0;
+    if (rd(&c, &l) != 0) return MVN_ERR_LAUNCH;
+    if (c && !*count) *first_line = l;
+    *count += c;
+  }
+  return MVN_OK;
+}
+
 extern "C" int mvn_debug_set_unproject(int lds_slots, int kernel) {
   if (lds_slots < 0 || kernel < 0 || kernel > 2) return MVN_ERR_ARG;
   mvn::g_lds_slots.store(lds_slots, std::memory_order_relaxed);

@@ -248,6 +248,7 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
         float q[G];
 #pragma unroll
         for (int k = 0; k < G; ++k) q[k] = (in && c0 + k < C) ? ldf(fb, (size_t(v) * C + c0 + k) * HW + size_t(gy) * W + gx) : 0.f;
+        MVN_DASSERT(idx >= 0 && idx < kZero);
         fstage[idx] = make_float4(q[0], q[1], q[2], q[3]);
       }
     }
@@ -269,6 +270,7 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
       if constexpr (kNeedSamples) {
         if (v < N) {
           const int o = slot[v], o2 = has[v] ? slot[v] + rpitch[v] : kZero;
+          MVN_DASSERT(o >= 0 && o + 1 < kSlots && o2 >= 0 && o2 + 1 < kSlots);
           const float4 a = fstage[o], bq = fstage[o + 1], c = fstage[o2], d = fstage[o2 + 1];
           const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {bq.x, bq.y, bq.z, bq.w};
           const float cv[4] = {c.x, c.y, c.z, c.w}, dv[4] = {d.x, d.y, d.z, d.w};

@@ -452,6 +452,7 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
         uint32_t bits[G];
 #pragma unroll
         for (int k = 0; k < G; ++k) bits[k] = buf_load<TIn>(frs, go, uint32_t((c0 + k) * HW * int(sizeof(TIn))));
+        MVN_DASSERT(idx >= 0 && idx < kZeroSlot);
         stage[idx] = pack<TIn>(bits);
       }
       __syncthreads();

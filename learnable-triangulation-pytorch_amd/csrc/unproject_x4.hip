@@ -303,6 +303,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     }
     npass = too_big ? -1 : pass + 1;
     total = chunks0;
+    MVN_DASSERT(too_big || (total <= MC * kThreads && snext <= lim));
   }
 
   if (npass < 0) {
@@ -330,6 +331,9 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       const int slot = rv.sbase + dy * rv.pitch + dx;
       anw[v] = uint32_t(use ? slot : kZeroSlot) * kSlotB;
       asw[v] = uint32_t(use ? slot + rv.pitch : kZeroSlot) * kSlotB;
+      // the four taps (and the east neighbour of the zero slot) lie inside one buffer
+      MVN_DASSERT(!use || (dx >= 0 && dy >= 0 && dx + 1 < rv.bw && dy + 1 < rv.bh &&
+                           slot + rv.pitch + 1 < kTrash));
     }
   };
   // Chunk (k of a pass) -> global byte offset (kOob outside the image), first LDS slot and
@@ -365,6 +369,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
         q = make_uint4(chunk_px(pre[0], p), chunk_px(pre[1], p), chunk_px(pre[2], p), chunk_px(pre[3], p));
       else
         q = make_uint2(chunk_px(pre[0], p), chunk_px(pre[1], p));
+      MVN_DASSERT(!(mask & (1u << p)) || (s0 + p >= 0 && s0 + p < kTrash));   // a box slot, not trash / zero
       if constexpr (sizeof(TIn) == 2 || G == 2)
         buf[(mask & (1u << p)) ? s0 + p : kTrash + lane] = q;
       else if (mask & (1u << p))

@@ -106,6 +106,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
       for (int u = 0; u < kBatch; ++u) {
         const int q = t + (i0 + u) * kThreads;
+        MVN_DASSERT(q >= total || (chunk_dst(-PAD, q) >= 0 && chunk_dst(-PAD, q) < HVOX * 4));
         if (q < total) halo[chunk_dst(-PAD, q)] = vals[u];
       }
     }
@@ -299,6 +300,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
         if (d & 1u) {
           int slot = ((gxn + PAD) % HX) + int((d >> 1) & 3u);
           if (slot >= HX) slot -= HX;
+          MVN_DASSERT(slot * kSliceChunks + int((d >> 3) & 1023u) < HVOX * 4);
           halo[slot * kSliceChunks + int((d >> 3) & 1023u)] = sv[u];
         }
       }

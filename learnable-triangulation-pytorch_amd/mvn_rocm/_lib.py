@@ -10,7 +10,10 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmvn_hip.so")
+# MVN_HIP_LIB selects another in-tree build, e.g. the debug build with device-side assertions
+# (``make -C learnable-triangulation-pytorch_amd debug`` -> libmvn_hip_debug.so); read once, at
+# import — never on a launch path
+LIB_PATH = os.path.abspath(os.environ.get("MVN_HIP_LIB") or os.path.join(_HERE, "libmvn_hip.so"))
 
 MVN_OK = 0
 MVN_DTYPE_F32 = 0
@@ -61,6 +64,8 @@ SIGNATURES = {
                                   + [_c_int] * 5 + [_c_void_p]),
     "mvn_dlt_backward": (_c_int, [_c_void_p] * 6 + [_c_int, _c_int, _c_int, _c_void_p]),
     "mvn_debug_set_unproject": (_c_int, [_c_int, _c_int]),
+    "mvn_debug_device_asserts": (_c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint),
+                                          ctypes.POINTER(ctypes.c_uint)]),
     "mvn_debug_unproject_occupancy": (_c_int, [_c_int]),
 }
 
@@ -109,3 +114,15 @@ class unproject_knobs:
     def __exit__(self, *exc):
         check(load().mvn_debug_set_unproject(0, 0), "mvn_debug_set_unproject")
         return False
+
+
+def device_asserts():
+    """(enabled, failures, first failing source line) of the debug build's device-side
+    assertions since the last call (the counters are cleared); enabled is False for the
+    release build.  Synchronises the current device first."""
+    import torch
+    torch.cuda.synchronize()
+    en, cnt, line = ctypes.c_int(0), ctypes.c_uint(0), ctypes.c_uint(0)
+    check(load().mvn_debug_device_asserts(ctypes.byref(en), ctypes.byref(cnt), ctypes.byref(line)),
+          "mvn_debug_device_asserts")
+    return bool(en.value), int(cnt.value), int(line.value)

@@ -25,6 +25,25 @@ def golden():
     return load_golden
 
 
+@pytest.fixture(autouse=True)
+def _device_asserts(request):
+    """With the debug library loaded (MVN_HIP_LIB=.../libmvn_hip_debug.so, `make debug`), fail
+    a GPU test whose kernels tripped a device-side assertion (csrc/common.hpp MVN_DASSERT:
+    index / layout invariants, counted instead of trapping)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    from mvn_rocm import _lib
+    if _lib._lib is None:
+        return
+    import torch
+    if not torch.cuda.is_available():
+        return
+    enabled, count, line = _lib.device_asserts()
+    if enabled:
+        assert count == 0, f"{count} device-side assertion failure(s), the first at source line {line}"
+
+
 @pytest.fixture(scope="session")
 def device():
     import torch

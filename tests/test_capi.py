@@ -43,6 +43,23 @@ def test_every_declared_symbol_is_exported(lib):
         getattr(lib, name)
 
 
+def test_debug_build_exports_the_same_symbols_and_reports_itself(lib):
+    """The debug build (device-side assertions, `make debug`) is a drop-in for the release
+    library: the same C ABI; mvn_debug_device_asserts says which build it is."""
+    import ctypes
+    from mvn_rocm import _lib
+    dbg = os.path.join(os.path.dirname(_lib.__file__), "libmvn_hip_debug.so")
+    if not os.path.exists(dbg):
+        pytest.skip("debug library not built (make -C learnable-triangulation-pytorch_amd debug)")
+    out = subprocess.run(["nm", "-D", "--defined-only", dbg], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT\s+(mvn_\w+)", out))
+    assert set(header_functions()) <= exported
+    en, cnt, line = ctypes.c_int(7), ctypes.c_uint(7), ctypes.c_uint(7)
+    assert lib.mvn_debug_device_asserts(ctypes.byref(en), ctypes.byref(cnt), ctypes.byref(line)) == 0
+    assert (en.value, cnt.value, line.value) == (0, 0, 0)          # release build: no checks compiled in
+    assert lib.mvn_debug_device_asserts(None, ctypes.byref(cnt), ctypes.byref(line)) == -1
+
+
 def test_version_and_errors(lib):
     assert lib.mvn_version() == (0 << 16) | (1 << 8)
     for code in (0, -1, -2, -3, -4, -5):

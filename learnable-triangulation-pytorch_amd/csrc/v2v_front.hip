@@ -175,9 +175,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
     // loop back-edge the compiler drains every load (more LDS reads are in flight than
     // lgkmcnt counts) and shuffles accumulators.
     uint4 A[TX][HY];
+    // local x-row x of this wave <-> output x-row (w + x) & 3: every wave's own row is its
+    // local row 0, so the last pass and the final sum need no per-wave code copies (a switch
+    // on w made the compiler shuffle the 64 accumulators between register assignments)
     auto a_addr = [&](int q, int x) {
       const int dx = q / KS, dz = q - dx * KS;
-      int slot = (x0 + dx) % HX + x;                        // halo x = dx + x  <->  gx = x0 - PAD + dx + x
+      int slot = (x0 + dx) % HX + ((w + x) & 3);            // halo x = dx + row  <->  gx = x0 - PAD + dx + row
       if (slot >= HX) slot -= HX;
       return hbase + uint32_t(slot * HY * HZ * 64 + ((r + dz) * 4 + (kb ^ swz(r + dz))) * 16);
     };
@@ -192,7 +195,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
       const int wq = b_off(qn < 0 ? 0 : qn);
       const char* hb[TX];
 #pragma unroll
-      for (int x = 0; x < TX; ++x) hb[x] = a_addr(qn < 0 ? 0 : qn, NEXT_ONE ? w : x);
+      for (int x = 0; x < TX; ++x) hb[x] = a_addr(qn < 0 ? 0 : qn, NEXT_ONE ? 0 : x);
 #pragma unroll
       for (int hy = 0; hy < HY; ++hy) {
         __builtin_amdgcn_sched_barrier(0);
@@ -248,12 +251,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
         for (int u = 2 * i; u < 2 * i + 2 && u < kStage; ++u) sv[u] = ld_chunk(more ? stage_src(u, gxn) : kOob);
       }
     }
-    switch (w) {                              // pass 48, own x-row
-      case 0: pass(-1, T{}, std::integral_constant<int, 0>{}); break;
-      case 1: pass(-1, T{}, std::integral_constant<int, 1>{}); break;
-      case 2: pass(-1, T{}, std::integral_constant<int, 2>{}); break;
-      default: pass(-1, T{}, std::integral_constant<int, 3>{}); break;
-    }
+    pass(-1, T{}, std::integral_constant<int, 0>{});   // pass 48, own x-row (local row 0)
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- partial sums: wave k owns output x-row k.  The 4 slots of slices x0-3 .. x0 are
@@ -269,28 +267,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
     };
     __syncthreads();                          // every wave is done with the halo
 #pragma unroll
-    for (int k = 0; k < TX; ++k)
-      if (k != w) {
-        const int j = w < k ? w : w - 1;
+    for (int x = 1; x < TX; ++x) {
+      const int k = (w + x) & 3, j = w < k ? w : w - 1;
 #pragma unroll
-        for (int m = 0; m < TY; ++m) *red_addr(k, j, m) = acc[k][m];
-      }
+      for (int m = 0; m < TY; ++m) *red_addr(k, j, m) = acc[x][m];
+    }
     __syncthreads();
     f32x4_t sum[TY];
-    auto gather = [&](auto own) {
-      constexpr int K = decltype(own)::value;
 #pragma unroll
-      for (int m = 0; m < TY; ++m) {
-        sum[m] = acc[K][m];
+    for (int m = 0; m < TY; ++m) {
+      sum[m] = acc[0][m];
 #pragma unroll
-        for (int j = 0; j < kWaves - 1; ++j) sum[m] += *red_addr(K, j, m);
-      }
-    };
-    switch (w) {
-      case 0: gather(std::integral_constant<int, 0>{}); break;
-      case 1: gather(std::integral_constant<int, 1>{}); break;
-      case 2: gather(std::integral_constant<int, 2>{}); break;
-      default: gather(std::integral_constant<int, 3>{}); break;
+      for (int j = 0; j < kWaves - 1; ++j) sum[m] += *red_addr(w, j, m);
     }
     __syncthreads();                          // the dead slots are read: the next slices go in
     if (more) {

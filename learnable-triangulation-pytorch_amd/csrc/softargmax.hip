@@ -149,7 +149,11 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
   constexpr int kPartChunk = kPartChunkT<T>;
   constexpr int RUNS = kPartChunk / (kWave * VEC);
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const int chunk = blockIdx.x * (kSaBlock / kWave) + wid, b = blockIdx.y;
+  // frames in DESCENDING order: the unprojection just wrote (and read the coordinates of) the
+  // last frames, which the 256 MiB MALL still holds; pass 1 then leaves the first frames there
+  // for the finalize, which walks them in ascending order (config 3 soft-argmax 182.9 -> 169.6 us
+  // inside the bench step, bit-identical; profiles/r17_ab_sa_rev.txt)
+  const int chunk = blockIdx.x * (kSaBlock / kWave) + wid, b = int(gridDim.y) - 1 - int(blockIdx.y);
   // joints [ja, jb) of this wave: gridDim.z splits the joints when the frames alone give too
   // few waves to fill the chip (config 2: 8 frames x 256 chunks = 2 waves per SIMD)
   const int jn = (J + int(gridDim.z) - 1) / int(gridDim.z), ja = int(blockIdx.z) * jn, jb = min(J, ja + jn);

@@ -315,6 +315,12 @@ int mvn_debug_set_unproject(int lds_slots, int kernel);
 int mvn_debug_device_asserts(int* enabled, unsigned* count, unsigned* first_line);
 
 /*
+ * Self-test of the device-side assertions: one 64-lane launch whose lanes >= n fail a check
+ * (64 - n failures in the debug build, none in the release build).  0 <= n <= 64.
+ */
+int mvn_debug_dassert_selftest(int n, void* stream);
+
+/*
  * Diagnostics: workgroups of the four-view unprojection kernel resident per CU (its LDS and
  * register budget; the persistent grid is this x the CU count), for f32 (bf16_maps = 0) or
  * bf16 (1) feature maps.  Needs a device; returns a count >= 1.

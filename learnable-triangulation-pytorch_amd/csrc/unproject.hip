@@ -234,6 +234,19 @@ std::vector<DassertReader>& dassert_registry() {
 }
 }  // namespace mvn
 
+namespace mvn {
+namespace {
+// one deliberately failing check per lane >= n (the mechanism's self-test)
+__global__ void dassert_selftest(int n) { MVN_DASSERT(int(threadIdx.x) < n); }
+}  // namespace
+}  // namespace mvn
+
+extern "C" int mvn_debug_dassert_selftest(int n, void* stream) {
+  if (n < 0 || n > 64) return MVN_ERR_ARG;
+  mvn::dassert_selftest<<<1, 64, 0, static_cast<hipStream_t>(stream)>>>(n);
+  return mvn::launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
+}
+
 extern "C" int mvn_debug_device_asserts(int* enabled, unsigned* count, unsigned* first_line) {
   if (!enabled || !count || !first_line) return MVN_ERR_ARG;
 #ifdef MVN_DEVICE_ASSERTS

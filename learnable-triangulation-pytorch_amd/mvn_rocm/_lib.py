@@ -66,6 +66,7 @@ SIGNATURES = {
     "mvn_debug_set_unproject": (_c_int, [_c_int, _c_int]),
     "mvn_debug_device_asserts": (_c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint),
                                           ctypes.POINTER(ctypes.c_uint)]),
+    "mvn_debug_dassert_selftest": (_c_int, [_c_int, _c_void_p]),
     "mvn_debug_unproject_occupancy": (_c_int, [_c_int]),
 }
 

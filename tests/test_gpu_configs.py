@@ -369,3 +369,20 @@ def test_channels_last_entry_points_empty_batch_and_many_views(device):
     y = v2v.unproject_v2v_front(feat, P, coords, packed, scale, shift)
     two = v2v.v2v_front(v2v.unproject_channels_last(feat, P, coords, "softmax"), packed, scale, shift)
     assert torch.equal(y, two)
+
+
+def test_device_assertions_count_and_clear(device):
+    """The debug build's device-side assertions (csrc/common.hpp MVN_DASSERT) count failures
+    without trapping and report the failing line; the release build compiles them away.
+    Run with MVN_HIP_LIB=.../libmvn_hip_debug.so for the debug half."""
+    from mvn_rocm import _lib
+    lib = _lib.load()
+    enabled, count, _ = _lib.device_asserts()          # clear anything earlier
+    assert count == 0
+    _lib.check(lib.mvn_debug_dassert_selftest(40, torch.cuda.current_stream().cuda_stream), "selftest")
+    enabled, count, line = _lib.device_asserts()
+    if enabled:
+        assert count == 24 and line > 0
+        assert _lib.device_asserts()[1] == 0            # read-and-clear
+    else:
+        assert (count, line) == (0, 0)

@@ -7,7 +7,8 @@
 // Here one lane owns one (b, j):
 //   1. rows of A are formed in f32 exactly as multiview.py:150-152 forms them
 //      (A = P[2]*pt; A -= P[:2]; A *= conf — three separately rounded ops),
-//   2. each row is folded into a 4x4 upper-triangular R by Givens rotations (f64),
+//   2. each row is folded into a 4x4 upper-triangular R by Givens rotations (f64,
+//      Newton-refined hardware reciprocal square roots: round 3, config 1 latency),
 //      so R^T R = A^T A without ever squaring the condition number and for any N,
 //   3. a one-sided Jacobi SVD of R (f64) gives the right singular vectors; the one
 //      of the smallest singular value is the homogeneous point (multiview.py:154-156),
@@ -19,13 +20,35 @@ namespace {
 
 constexpr int kDltBlock = 64;
 
+// f64 reciprocal and reciprocal square root: the hardware estimates (v_rcp_f64 / v_rsq_f64,
+// about half the mantissa) refined by two Newton steps (fma): within an ulp or two of the IEEE
+// result, in ~5 dependent operations instead of the ~10-20 of IEEE '/', sqrt and hypot.  The
+// solve is one lane's serial f64 chain, so its latency is the kernel's time (config 1).
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
+  return __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
+}
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double h = 0.5 * y, g = x * y;
+    y = __builtin_fma(y, __builtin_fma(-g, h, 0.5), y);   // y (1.5 - x y^2 / 2)
+  }
+  return y;
+}
+
+// Fold row a into the upper-triangular R: one Givens rotation per non-zero entry
+// (r = |(R_kk, a_k)|, c = R_kk / r, s = a_k / r from one reciprocal square root).
 __device__ __forceinline__ void givens_fold(double (&R)[4][4], double (&a)[4]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (a[k] == 0.0) continue;
-    const double r = hypot(R[k][k], a[k]);
-    const double c = R[k][k] / r, s = a[k] / r;
-    R[k][k] = r;
+    const double n2 = __builtin_fma(R[k][k], R[k][k], a[k] * a[k]);
+    const double ri = rsqrt_nr(n2);
+    const double c = R[k][k] * ri, s = a[k] * ri;
+    R[k][k] = n2 * ri;
     a[k] = 0.0;
 #pragma unroll
     for (int l = k + 1; l < 4; ++l) {
@@ -37,6 +60,7 @@ __device__ __forceinline__ void givens_fold(double (&R)[4][4], double (&a)[4]) {
 }
 
 // One-sided Jacobi on the columns of U (= R on entry); V accumulates the rotations.
+// Convergence test |gamma| <= 1e-15 sqrt(alpha beta) as gamma^2 <= 1e-30 alpha beta (no sqrt).
 __device__ __forceinline__ void jacobi_svd(double (&U)[4][4], double (&V)[4][4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -55,11 +79,13 @@ __device__ __forceinline__ void jacobi_svd(double (&U)[4][4], double (&V)[4][4])
           beta += U[i][q] * U[i][q];
           gamma += U[i][p] * U[i][q];
         }
-        if (gamma == 0.0 || fabs(gamma) <= 1e-15 * sqrt(alpha * beta)) continue;
+        if (gamma == 0.0 || gamma * gamma <= 1e-30 * (alpha * beta)) continue;
         rotated = true;
-        const double zeta = (beta - alpha) / (2.0 * gamma);
-        const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-        const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+        const double zeta = (beta - alpha) * rcp_nr(2.0 * gamma);
+        const double z2 = __builtin_fma(zeta, zeta, 1.0);
+        const double root = z2 * rsqrt_nr(z2);                       // sqrt(1 + zeta^2)
+        const double t = (zeta >= 0.0 ? 1.0 : -1.0) * rcp_nr(fabs(zeta) + root);
+        const double c = rsqrt_nr(__builtin_fma(t, t, 1.0)), s = c * t;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const double up = U[i][p], uq = U[i][q];

@@ -84,7 +84,10 @@ __device__ __forceinline__ void jacobi_svd(double (&U)[4][4], double (&V)[4][4])
         const double zeta = (beta - alpha) * rcp_nr(2.0 * gamma);
         const double z2 = __builtin_fma(zeta, zeta, 1.0);
         const double root = z2 * rsqrt_nr(z2);                       // sqrt(1 + zeta^2)
-        const double t = (zeta >= 0.0 ? 1.0 : -1.0) * rcp_nr(fabs(zeta) + root);
+        // |zeta| > 1e150: zeta^2 overflows (inf * rsqrt(inf) = NaN); there t = 1 / (2 zeta) to
+        // working precision, which is what the IEEE form tends to
+        const double t = fabs(zeta) > 1e150 ? 0.5 * rcp_nr(zeta)
+                                            : (zeta >= 0.0 ? 1.0 : -1.0) * rcp_nr(fabs(zeta) + root);
         const double c = rsqrt_nr(__builtin_fma(t, t, 1.0)), s = c * t;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {

@@ -10,8 +10,9 @@
 //   2. each row is folded into a 4x4 upper-triangular R by Givens rotations (f64,
 //      Newton-refined hardware reciprocal square roots: round 3, config 1 latency),
 //      so R^T R = A^T A without ever squaring the condition number and for any N,
-//   3. a one-sided Jacobi SVD of R (f64) gives the right singular vectors; the one
-//      of the smallest singular value is the homogeneous point (multiview.py:154-156),
+//   3. the right singular vector of the smallest singular value is the homogeneous point
+//      (multiview.py:154-156): inverse iteration on R^T R (2-3 steps), or, when that does
+//      not converge (near-equal smallest singular values), a one-sided Jacobi SVD of R (f64),
 //   4. X[:3] / X[3] (multiview.py:157; sign of the null vector cancels).
 #include "common.hpp"
 
@@ -103,6 +104,66 @@ __device__ __forceinline__ void jacobi_svd(double (&U)[4][4], double (&V)[4][4])
   }
 }
 
+// Null vector by inverse iteration on R^T R = A^T A (its eigenvector of the smallest eigenvalue,
+// the right singular vector multiview.py:154-156 takes): two triangular solves per step, each
+// vector rescaled by its largest entry and the result normalised.  The null component grows by
+// (sigma_2 / sigma_min)^2 per step: at the bench and test geometries 4-6 steps reach a step
+// change below 1e-10 (results within 2e-13 of the f64 LAPACK restatement, numpy model); still
+// moving after 12 steps (near-equal smallest singular values) returns false and the caller
+// runs the Jacobi SVD instead.  A zero
+// pivot (an exact null vector) is replaced by 1e-30 of the largest one.
+__device__ __forceinline__ bool inverse_iteration(const double (&R)[4][4], double (&x)[4]) {
+  double dmax = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) dmax = fmax(dmax, fabs(R[k][k]));
+  if (!(dmax > 0.0)) return false;
+  double rinv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double d = R[k][k];
+    rinv[k] = rcp_nr(fabs(d) > 1e-30 * dmax ? d : (d < 0.0 ? -1e-30 : 1e-30) * dmax);
+  }
+  auto rescale = [](double (&v)[4]) {
+    const double m = fmax(fmax(fabs(v[0]), fabs(v[1])), fmax(fabs(v[2]), fabs(v[3])));
+    const double r = rcp_nr(m);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] *= r;
+  };
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x[i] = 0.5;
+  for (int it = 0; it < 12; ++it) {
+    double z[4], y[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {                 // R^T z = x (forward substitution)
+      double acc = x[k];
+#pragma unroll
+      for (int i = 0; i < k; ++i) acc = __builtin_fma(-R[i][k], z[i], acc);
+      z[k] = acc * rinv[k];
+    }
+    rescale(z);
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {                // R y = z (back substitution)
+      double acc = z[k];
+#pragma unroll
+      for (int l = k + 1; l < 4; ++l) acc = __builtin_fma(-R[k][l], y[l], acc);
+      y[k] = acc * rinv[k];
+    }
+    rescale(y);
+    const double n = rsqrt_nr(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+    const double sg = (y[0] * x[0] + y[1] * x[1] + y[2] * x[2] + y[3] * x[3]) < 0.0 ? -n : n;
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      y[i] *= sg;
+      d += (y[i] - x[i]) * (y[i] - x[i]);
+      x[i] = y[i];
+    }
+    if (!(d == d)) return false;                  // NaN (non-finite input): the Jacobi path decides
+    if (it > 0 && d < 1e-20) return true;
+  }
+  return false;
+}
+
 __global__ __launch_bounds__(kDltBlock) void dlt_kernel(const float* __restrict__ P, const float* __restrict__ pts,
                                                         const float* __restrict__ conf, float* __restrict__ out,
                                                         int B, int N, int J) {
@@ -135,21 +196,23 @@ __global__ __launch_bounds__(kDltBlock) void dlt_kernel(const float* __restrict_
     }
   }
 
-  double V[4][4];
-  jacobi_svd(R, V);
-  int kmin = 0;
-  double smin = 0.0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const double n2 = R[0][k] * R[0][k] + R[1][k] * R[1][k] + R[2][k] * R[2][k] + R[3][k] * R[3][k];
-    if (k == 0 || n2 < smin) { smin = n2; kmin = k; }
-  }
   double X[4];
+  if (!inverse_iteration(R, X)) {
+    double V[4][4];
+    jacobi_svd(R, V);
+    int kmin = 0;
+    double smin = 0.0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    X[i] = V[i][0];
+    for (int k = 0; k < 4; ++k) {
+      const double n2 = R[0][k] * R[0][k] + R[1][k] * R[1][k] + R[2][k] * R[2][k] + R[3][k] * R[3][k];
+      if (k == 0 || n2 < smin) { smin = n2; kmin = k; }
+    }
 #pragma unroll
-    for (int k = 1; k < 4; ++k) if (kmin == k) X[i] = V[i][k];
+    for (int i = 0; i < 4; ++i) {
+      X[i] = V[i][0];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) if (kmin == k) X[i] = V[i][k];
+    }
   }
   float* o = out + size_t(t) * 3;
   o[0] = float(X[0] / X[3]);

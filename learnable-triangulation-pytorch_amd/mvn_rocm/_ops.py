@@ -25,7 +25,14 @@ _CODE_DTYPE = {v: k for k, v in _DTYPE_CODE.items()}
 
 
 def _stream(t: Tensor) -> int:
-    return torch.cuda.current_stream(t.device).cuda_stream
+    # the raw pointer of the device's current stream, without building a torch.cuda.Stream
+    # object per call (host cost per op: the small-batch algebraic path is launch-bound)
+    return torch._C._cuda_getCurrentRawStream(t.device.index)
+
+
+def f32c(t: Tensor) -> Tensor:
+    """t as contiguous float32, with no dispatcher round trip when it already is."""
+    return t if (t.dtype is torch.float32 and t.is_contiguous()) else t.float().contiguous()
 
 
 def _require_gpu(*tensors: Optional[Tensor]) -> None:

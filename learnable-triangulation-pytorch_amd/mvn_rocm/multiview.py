@@ -17,9 +17,9 @@ def triangulate_batch_of_points(proj_matricies_batch, points_batch, confidences_
     """
     if proj_matricies_batch.shape[:2] != points_batch.shape[:2]:   # multiview.py:143
         raise AssertionError("proj_matricies and points must have the same number of views")
-    proj = proj_matricies_batch.float().contiguous()
-    pts = points_batch.float().contiguous()
-    conf = None if confidences_batch is None else confidences_batch.float().contiguous()
+    proj = _ops.f32c(proj_matricies_batch)
+    pts = _ops.f32c(points_batch)
+    conf = None if confidences_batch is None else _ops.f32c(confidences_batch)
     if torch.is_grad_enabled() and (pts.requires_grad or (conf is not None and conf.requires_grad)):
         return DLTFunction.apply(proj, pts, conf)
     return _ops.call(_ops.dlt, proj, pts, conf)

@@ -53,8 +53,8 @@ def unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, method, cub
         feat = feat.float()
     if feat.dim() != 5:
         raise RuntimeError(f"heatmaps must be (B, N, C, H, W), got {tuple(feat.shape)}")
-    proj = proj_matricies.float().contiguous()
-    conf = vol_confidences.float().contiguous() if agg == _lib.MVN_AGG_CONF else None
+    proj = _ops.f32c(proj_matricies)
+    conf = _ops.f32c(vol_confidences) if agg == _lib.MVN_AGG_CONF else None
     if proj.shape[:2] != feat.shape[:2] or proj.shape[2:] != (3, 4):
         raise RuntimeError(f"proj_matricies shape {tuple(proj.shape)} does not match heatmaps {tuple(feat.shape)}")
     if conf is not None and conf.shape != feat.shape[:3]:
@@ -88,7 +88,7 @@ def unproject_heatmaps(heatmaps, proj_matricies, coord_volumes, volume_aggregati
             if _needs_grad(feat, conf):
                 return UnprojectCuboidFunction.apply(*args)
             return _ops.call(_ops.unproject_cuboid, *args)
-    coords = coord_volumes.float().contiguous()
+    coords = _ops.f32c(coord_volumes)
     if coords.dim() != 5 or coords.shape[0] != feat.shape[0] or coords.shape[4] != 3:
         raise RuntimeError(f"coord_volumes must be (B, Vx, Vy, Vz, 3), got {tuple(coords.shape)}")
     if _needs_grad(feat, conf):
@@ -124,7 +124,7 @@ def integrate_tensor_3d_with_coordinates(volumes, coord_volumes, softmax=True, *
             xyz, out = _ops.call(_ops.softargmax3d_cuboid, vol, cub.params, cub.transfer, bool(softmax),
                                  float(multiplier), bool(return_volumes), od)
         return xyz, (out if return_volumes else None)
-    coords = coord_volumes.float().contiguous()
+    coords = _ops.f32c(coord_volumes)
     if coords.shape != (vol.shape[0], Vx, Vy, Vz, 3):
         raise RuntimeError(f"coord_volumes {tuple(coords.shape)} does not match volumes {tuple(vol.shape)}")
     args = (vol, coords, bool(softmax), float(multiplier), bool(return_volumes), od)

@@ -408,3 +408,23 @@ def test_v2v_front_full_size_vs_torch_cpu(device):
     ref = torch.relu(F.conv3d(x, w, None, padding=3) * scale.cpu().view(1, -1, 1, 1, 1)
                      + shift.cpu().view(1, -1, 1, 1, 1))
     assert max_rel(y.cpu().numpy(), ref.numpy()) <= 1e-4
+
+
+@pytest.mark.parametrize("softmax", (True, False))
+@pytest.mark.parametrize("hw", ((96, 96), (20, 24), (37, 12), (112, 108)))
+def test_softargmax2d_register_path_vs_restatement(device, softmax, hw):
+    """The register-resident 2D soft-argmax (maps <= 12,288 pixels with W % 4 == 0, csrc/
+    softargmax2d.hip softargmax2d_reg): coordinates and returned maps against the float64
+    restatement of op.py:11-47, f32 and bf16, a last run of 4 pixels partly past the map
+    (37 x 12 = 444 pixels) and the largest map it takes (112 x 108 = 12,096)."""
+    H, W = hw
+    hm = torch.randn((3, 17, H, W), generator=torch.Generator().manual_seed(H * W)) * 3
+    for dt in (torch.float32, torch.bfloat16):
+        x = hm.to(dt)
+        ref_xy, ref_maps = restate_np.integrate_tensor_2d(x.float().numpy() * 1.3, softmax)
+        xy, maps = _op().integrate_tensor_2d(x.to(device), softmax, multiplier=1.3)
+        assert max_rel(xy.cpu().numpy(), ref_xy) <= 1e-5
+        if dt == torch.float32:
+            assert max_rel(maps.cpu().numpy(), ref_maps) <= 1e-5
+        else:
+            np.testing.assert_allclose(maps.float().cpu().numpy(), ref_maps, rtol=2 ** -8, atol=1e-30)

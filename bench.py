@@ -272,6 +272,8 @@ class Workload:
         self.ev = []
         self._pool = []
         self.last = None
+        self.gathered = None
+        self.starts = None      # first frame of every rank's shard (set by the caller)
 
     def reserve_events(self, n):
         """Pre-create the timing events of n timed steps, so that no Event is constructed
@@ -302,6 +304,7 @@ class Workload:
         self.last = (vol, xyz)
         if self.world > 1:      # the path's one exchange: joints of every rank, RCCL over xGMI
             xyz = mdist.gather_joints(xyz, self.global_batch)
+            self.gathered = xyz
         return xyz, sm
 
     def kernel_ms(self):
@@ -311,10 +314,11 @@ class Workload:
         return (sum(a.elapsed_time(b) for a, b, _ in self.ev) / n, sum(b.elapsed_time(c) for _, b, c in self.ev) / n)
 
 
-def run_config(name, args, rank, world, device, clock, cuboid=False, cfg=None, first_frame=None):
+def run_config(name, args, rank, world, device, clock, cuboid=False, cfg=None, first_frame=None, starts=None):
     import torch
     cfg = cfg if cfg is not None else _configs()[name]
     wl = Workload(cfg, rank, world, device, cuboid=cuboid, first_frame=first_frame)
+    wl.starts = starts if starts is not None else [r * cfg["frames"] for r in range(world)]
     wl.reserve_events(args.steps)
     elapsed = timed_loop(lambda t: wl.step(t), args, clock)
     E = 2 if cfg["dtype"] == torch.bfloat16 else 4
@@ -342,6 +346,7 @@ def run_config5(args, rank, world, device, clock, cuboid=False):
                                                   torch.randn(16, generator=g) * 0.1, torch.zeros(16), torch.ones(16),
                                                   device=device)
     ev = []
+    last = []
     coords = vb.cuboids(device) if cuboid else vb.coords
     # timing events created (first record) before the timed region, as Workload.reserve_events
     pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -359,6 +364,7 @@ def run_config5(args, rank, world, device, clock, cuboid=False):
         if timed:
             e1.record()
             ev.append((e0, e1))
+        last[:] = [cl, y]
         return y
 
     elapsed = timed_loop(step, args, clock)
@@ -368,7 +374,9 @@ def run_config5(args, rank, world, device, clock, cuboid=False):
     # through a 134 MB workspace instead of the 1.07 GB whole-batch intermediate)
     one = timed_loop(lambda t: v2v.unproject_v2v_front(vb.features, vb.proj, coords, packed, scale, shift, "softmax",
                                                        torch.bfloat16), args, clock)
-    return dict(workload=cfg["label"], value=B * world * args.steps / elapsed, unit="frames/s",
+    pin = None if cuboid else dict(feat=vb.features, proj=vb.proj, coords=vb.coords, last=tuple(last),
+                                   w_bf16=w.bfloat16().float(), scale=scale, shift=shift)
+    return dict(parity_inputs=pin, workload=cfg["label"], value=B * world * args.steps / elapsed, unit="frames/s",
                 one_call={"value": B * world * args.steps / one, "ms_per_step": one / args.steps * 1e3,
                           "api": "mvn_unproject_v2v_front (groups of 8 frames, MALL-resident intermediate)"},
                 ms_per_step=elapsed / args.steps * 1e3, frames_per_gpu=B, dtype="bf16",
@@ -486,48 +494,131 @@ def cpu_baseline(budget_s=8.0):
                                f"batch 1, 4 views x 17 joints, {threads} threads")
 
 
-def parity_check(res):
-    """Parity of the timed workload itself (SURVEY.md §5 'Metrics': the line carries the parity
-    error): frame 0 of the last timed step's unprojection and joints against the C oracle
+def _rel(a, b):
+    import numpy as np
+    return float(np.abs(a.astype(np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _within_one_bf16_ulp(got, ref, slack):
+    """Every value of a bf16 result within one bf16 ulp of the f32 reference (+ `slack` x
+    max|ref| absolute, where the f32 value cancels towards 0)."""
+    import numpy as np
+    ref = ref.astype(np.float64)
+    _, e = np.frexp(ref)
+    ulp = np.where(ref == 0, 0.0, np.ldexp(1.0, e - 8))
+    return bool((np.abs(got.astype(np.float64) - ref) <= ulp + slack * np.abs(ref).max()).all())
+
+
+def _frames(n):
+    """Frames of an n-frame launch the parity check recomputes: the first and the last (the
+    last frame's addresses are the launch's largest; at config 4's 128 frames its output
+    lies past 2^32 bytes)."""
+    return sorted({0, n - 1})
+
+
+def _np_feat(t):
+    import numpy as np
+    import torch
+    t = t.cpu()
+    return t.view(torch.int16).numpy().view(np.uint16) if t.dtype == torch.bfloat16 else t.numpy()
+
+
+def parity_unproject(feat, proj, coords, vol, J, frames, xyz=None, layout="ncdhw"):
+    """Frames `frames` of a timed unprojection (softmax agg) against the C oracle
     (oracle/mvn_oracle.c, pinned to the reference's goldens) on the same inputs.
-      unproject_max_rel    GPU volume vs oracle unproject_heatmaps (op.py:99-163), softmax agg;
-                           max|d| / max|ref| over the frame's C x 64^3 values
+      unproject_max_rel    GPU volume vs oracle unproject_heatmaps (op.py:99-163):
+                           max|d| / max|ref| over the frame's C x V^3 values
       joints_max_rel       GPU joints vs the oracle soft-argmax (op.py:84-96) of the GPU's own
-                           channels [0:17] (the same input the GPU's soft-argmax saw)
+                           channels [0:J] (the same input the GPU's soft-argmax saw)
       chain_joints_max_rel GPU joints vs the oracle chain unproject -> soft-argmax end to end
-    bf16 maps: the oracle runs in f32 on the same bf16 bits; the GPU writes a bf16 volume."""
+    bf16 maps: the oracle runs in f32 on the same bf16 bits; a bf16 volume is checked to be
+    within one bf16 ulp of it.  Worst value over the frames."""
     import numpy as np
     import torch
     from oracle import capi
+    out = dict(frames_checked=list(frames), unproject_max_rel=0.0)
+    bf16 = feat.dtype == torch.bfloat16
+    for f in frames:
+        fe = _np_feat(feat[f:f + 1])
+        pr, co = proj[f:f + 1].cpu().numpy(), coords[f:f + 1].cpu().numpy()
+        ref_vol = capi.unproject(fe, pr, co, "softmax", feat_bf16_bits=bf16)
+        got = vol[f:f + 1]
+        if layout == "ndhwc":
+            got = got.permute(0, 4, 1, 2, 3)
+        got_vol = got.float().cpu().numpy()
+        out["unproject_max_rel"] = max(out["unproject_max_rel"], _rel(got_vol, ref_vol))
+        if vol.dtype == torch.bfloat16:
+            ok = _within_one_bf16_ulp(got_vol, ref_vol, 1e-5)
+            out["unproject_within_one_bf16_ulp"] = out.get("unproject_within_one_bf16_ulp", True) and ok
+        if xyz is not None:
+            got_xyz = xyz[f:f + 1].cpu().numpy().astype(np.float64)
+            own_xyz, _ = capi.softargmax3d(np.ascontiguousarray(got_vol[:, :J]), co, True, 1.0)
+            ref_xyz, _ = capi.softargmax3d(np.ascontiguousarray(ref_vol[:, :J]), co, True, 1.0)
+            out["joints_max_rel"] = max(out.get("joints_max_rel", 0.0), _rel(got_xyz, own_xyz))
+            out["chain_joints_max_rel"] = max(out.get("chain_joints_max_rel", 0.0), _rel(got_xyz, ref_xyz))
+    return out
+
+
+def parity_check(res):
+    """Parity of a timed workload itself (SURVEY.md §5 'Metrics': the line carries the parity
+    error): the first and the last frame of the last timed step, recomputed by the C oracle
+    on the same inputs (parity_unproject).  The oracle is the checker only: this runs after
+    the timed regions and nothing it computes enters a timed number."""
     wl = res["workload"]
     vol, xyz = wl.last
-    J = wl.cfg["joints"]
-    bf16 = wl.feat.dtype == torch.bfloat16
-    feat = wl.feat[:1].cpu()
-    feat = feat.view(torch.int16).numpy().view(np.uint16) if bf16 else feat.numpy()
-    proj, coords = wl.proj[:1].cpu().numpy(), wl.coords[:1].cpu().numpy()
     t0 = time.perf_counter()
-    ref_vol = capi.unproject(feat, proj, coords, "softmax", feat_bf16_bits=bf16)
-    got_vol = vol[:1].float().cpu().numpy()
-    got_xyz = xyz[:1].cpu().numpy().astype(np.float64)
-    own_xyz, _ = capi.softargmax3d(np.ascontiguousarray(got_vol[:, :J]), coords, True, 1.0)
-    ref_xyz, _ = capi.softargmax3d(np.ascontiguousarray(ref_vol[:, :J]), coords, True, 1.0)
-
-    def rel(a, b):
-        return float(np.abs(a.astype(np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
-
-    out = {}
-    if vol.dtype == torch.bfloat16:
-        # bf16 volume: every value within one bf16 ulp of the f32 oracle (+ the softmax's 1e-5
-        # f32 tolerance, where the aggregate cancels towards 0)
-        _, e = np.frexp(ref_vol.astype(np.float64))
-        ulp = np.where(ref_vol == 0, 0.0, np.ldexp(1.0, e - 8))
-        out["unproject_within_one_bf16_ulp"] = bool(
-            (np.abs(got_vol.astype(np.float64) - ref_vol) <= ulp + 1e-5 * np.abs(ref_vol).max()).all())
-    return dict(out, unproject_max_rel=rel(got_vol, ref_vol), joints_max_rel=rel(got_xyz, own_xyz),
-                chain_joints_max_rel=rel(got_xyz, ref_xyz), frames_checked=1,
-                bars="unproject <= 1e-5 (f32 out) / one bf16 ulp (bf16 out); joints <= 1e-4 (north_star)",
+    out = parity_unproject(wl.feat, wl.proj, wl.coords, vol, wl.cfg["joints"], _frames(vol.shape[0]), xyz)
+    return dict(out, bars="unproject <= 1e-5 (f32 out) / one bf16 ulp (bf16 out); joints <= 1e-4 (north_star)",
                 oracle="oracle/mvn_oracle.c via oracle/capi.py", oracle_s=time.perf_counter() - t0)
+
+
+def parity_check5(r5):
+    """Config 5's timed outputs, first and last frame: the channels-last bf16 unprojection
+    against the C oracle (within one bf16 ulp), and the V2V front block (bf16 out) against
+    torch's CPU conv3d on the same bf16 operands (the GPU's own unprojection and the
+    bf16-rounded weights, f32 math) + the folded BatchNorm + ReLU (v2v.py:7-17): within one
+    bf16 ulp + 1e-4 x max|ref|."""
+    import torch
+    import torch.nn.functional as F
+    p = r5["parity_inputs"]
+    cl, y = p["last"]
+    frames = _frames(cl.shape[0])
+    t0 = time.perf_counter()
+    out = parity_unproject(p["feat"], p["proj"], p["coords"], cl, 0, frames, layout="ndhwc")
+    w, sc, sh = p["w_bf16"], p["scale"].cpu().view(1, -1, 1, 1, 1), p["shift"].cpu().view(1, -1, 1, 1, 1)
+    conv_rel, conv_ok = 0.0, True
+    for f in frames:
+        x = cl[f:f + 1].permute(0, 4, 1, 2, 3).float().cpu()
+        ref = torch.relu(F.conv3d(x, w, None, padding=3) * sc + sh).numpy()
+        got = y[f:f + 1].float().cpu().numpy()
+        conv_rel = max(conv_rel, _rel(got, ref))
+        conv_ok = conv_ok and _within_one_bf16_ulp(got, ref, 1e-4)
+    return dict(out, v2v_front_max_rel=conv_rel, v2v_front_within_one_bf16_ulp_plus_1e4=conv_ok,
+                bars="unproject one bf16 ulp; v2v front one bf16 ulp + 1e-4 x max|ref| vs torch-CPU conv3d",
+                oracle="oracle/mvn_oracle.c via oracle/capi.py; torch.nn.functional.conv3d (CPU, f32)",
+                oracle_s=time.perf_counter() - t0)
+
+
+def verify_gather(res):
+    """world > 1: the gathered joints of the last timed step (RCCL all-gather) against the
+    first frame of every rank's shard recomputed on rank 0 from (seed, global frame index):
+    bit for bit (frames are independent in every kernel, so a frame's joints do not depend on
+    the batch it ran in).  Run after every timed region."""
+    import torch
+    from mvn_rocm import op, synth
+    wl = res["workload"]
+    c, got = wl.cfg, wl.gathered
+    if got is None:
+        return None
+    checked, ok = [], True
+    for start in wl.starts:
+        vb = synth.volumetric_batch(1, n_views=c["views"], channels=c["channels"], heatmap=c["heatmap"],
+                                    volume=c["volume"], dtype=c["dtype"], device=wl.device, seed=0, first_frame=start)
+        vol = op.unproject_heatmaps(vb.features, vb.proj, vb.coords, "softmax")
+        xyz, _ = op.integrate_tensor_3d_with_coordinates(vol[:, :c["joints"]], vb.coords, True)
+        ok = ok and bool(torch.equal(xyz[0], got[start]))
+        checked.append(start)
+    return dict(gather_verified=ok, frames_recomputed=checked)
 
 
 # ----------------------------------------------------------------------------- dry run (CPU)
@@ -637,7 +728,8 @@ def main():
         from mvn_rocm import dist as mdist
         start, count = mdist.shard(128, world, rank)
         c4 = dict(configs["4"], frames=count)
-        r4 = run_config("4", args, rank, world, device, clock, cfg=c4, first_frame=start)
+        r4 = run_config("4", args, rank, world, device, clock, cfg=c4, first_frame=start,
+                        starts=[mdist.shard(128, world, q)[0] for q in range(world)])
         cfg4 = dict(workload=c4["label"] + ", global batch 128 split over the ranks", value=128 * args.steps / r4["elapsed"],
                     unit="frames/s", scaling="strong", global_batch=128, frames_per_gpu=count,
                     ms_per_step=r4["ms_per_step"], unproject_ms=r4["unproject_ms"],
@@ -657,6 +749,17 @@ def main():
         parity = parity_check(main_res)
         if secondary is not None:
             secondary["parity"] = parity_check(sec_res)
+        if cfg4 is not None:
+            cfg4["parity"] = parity_check(r4)
+        if cfg5 is not None and cfg5.get("parity_inputs") is not None:
+            cfg5["parity"] = parity_check5(cfg5)
+    if cfg5 is not None:
+        cfg5.pop("parity_inputs", None)
+    gather = None
+    if rank == 0 and world > 1:
+        gather = verify_gather(main_res)
+        if cfg4 is not None:
+            cfg4["gather"] = verify_gather(r4)
 
     if rank == 0:
         r, c = main_res, main_res["cfg"]
@@ -684,6 +787,7 @@ def main():
             "path_frac": r["path_gbps"] / HBM_PEAK_GBPS,
             "cpu_baseline": base,
             "parity": parity,
+            "gather": gather,
             "secondary": secondary,
             "config1": config1,
             "in_kernel_coords": in_kernel_coords,

@@ -63,9 +63,22 @@ def _op(name: str):
     return deco
 
 
+def _tracing() -> bool:
+    """Something records or transforms the call: torch.compile, a torch-dispatch mode,
+    torch.jit.trace, or a functorch transform (vmap / grad / jvp wrap storage-less tensors)."""
+    if torch.compiler.is_compiling() or torch._C._len_torch_dispatch_stack():
+        return True
+    if torch._C._get_tracing_state() is not None:
+        return True
+    try:
+        return torch._C._functorch.peek_interpreter_stack() is not None
+    except AttributeError:        # older torch: no functorch interpreter stack
+        return False
+
+
 def call(op, *args):
     """op(*args) — through the dispatcher only while something traces."""
-    if torch.compiler.is_compiling() or torch._C._len_torch_dispatch_stack():
+    if _tracing():
         return op(*args)
     return op.eager(*args)
 

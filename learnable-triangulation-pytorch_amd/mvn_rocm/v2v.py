@@ -77,9 +77,11 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
         # the channels-last kernels take N <= 8 views (mvn_hip.h): more views go through the
         # NCDHW unprojection (any N) and one permute on the device
         from .op import unproject_heatmaps
-        vol = unproject_heatmaps(feat, proj, coord_volumes, volume_aggregation_method, align_corners=align_corners)
-        # f32 -> bf16 rounds to nearest even, as the kernels' own bf16 stores do
-        return vol.permute(0, 2, 3, 4, 1).to(out_dtype).contiguous()
+        # written in out_dtype by the kernel itself (bf16 maps into an f32 volume keep f32
+        # precision; an f32 volume is rounded to bf16 by the kernel's own nearest-even stores)
+        vol = unproject_heatmaps(feat, proj, coord_volumes, volume_aggregation_method, align_corners=align_corners,
+                                 out_dtype=out_dtype)
+        return vol.permute(0, 2, 3, 4, 1).contiguous()
     if cub is not None:
         # coordinates formed in-kernel from the per-frame cuboids (bit-identical)
         cub = coord_volumes

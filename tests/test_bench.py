@@ -41,3 +41,66 @@ def test_bench_a_failing_rank_ends_the_job():
                         "--dry-run-fail-rank", "1"], capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def _verify_worker(rank, world, port, out_path):
+    """One rank of a world-2 gloo job: its shard's joints (stand-in ops: the C oracle) are
+    all-gathered, then rank 0 runs bench.verify_gather — the check a multi-GPU bench line
+    carries as `gather` — against the true gather and against one with a corrupted frame."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    for p in (ROOT, os.path.join(ROOT, "learnable-triangulation-pytorch_amd")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from mvn_rocm import dist as mdist, op, synth
+    from oracle import capi
+
+    def unproject(feat, proj, coords, agg):          # stand-ins on the CPU: the C oracle
+        return torch.from_numpy(capi.unproject(feat.numpy(), proj.numpy(), coords.numpy(), agg))
+
+    def softargmax(vol, coords, softmax=True):
+        xyz, sm = capi.softargmax3d(np.ascontiguousarray(vol.numpy()), coords.numpy(), softmax, 1.0)
+        return torch.from_numpy(xyz), torch.from_numpy(sm)
+
+    op.unproject_heatmaps, op.integrate_tensor_3d_with_coordinates = unproject, softargmax
+    cfg = dict(frames=3, views=3, channels=4, heatmap=16, volume=8, joints=3, dtype=torch.float32)
+    G = 5
+    start, count = mdist.shard(G, world, rank)
+    vb = synth.volumetric_batch(count, n_views=3, channels=4, heatmap=16, volume=8, seed=0, first_frame=start)
+    xyz, _ = softargmax(unproject(vb.features, vb.proj, vb.coords, "softmax")[:, :3], vb.coords)
+    gathered = mdist.gather_joints(xyz.contiguous(), G)
+
+    class WL:
+        pass
+    wl = WL()
+    wl.cfg, wl.device, wl.gathered = cfg, torch.device("cpu"), gathered
+    wl.starts = [mdist.shard(G, world, q)[0] for q in range(world)]
+    if rank == 0:
+        good = bench.verify_gather({"workload": wl})
+        wl.gathered = gathered.clone()
+        wl.gathered[wl.starts[-1], 0, 0] += 1.0
+        bad = bench.verify_gather({"workload": wl})
+        with open(out_path, "w") as f:
+            json.dump([good, bad], f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_verify_gather_world2(tmp_path):
+    """bench.verify_gather: at world 2 over gloo, rank 0 recomputes the
+    first frame of every shard and compares it bit for bit with the all-gathered joints."""
+    import socket
+
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "verify.json")
+    mp.spawn(_verify_worker, args=(2, port, out), nprocs=2, join=True)
+    good, bad = json.load(open(out))
+    assert good == {"gather_verified": True, "frames_recomputed": [0, 3]}
+    assert bad["gather_verified"] is False

@@ -358,6 +358,12 @@ def test_channels_last_entry_points_empty_batch_and_many_views(device):
     cl = v2v.unproject_channels_last(feat, P, coords, "sum", out_dtype=torch.float32)
     ref = op.unproject_heatmaps(feat, P, coords, "sum")
     assert torch.equal(cl, ref.permute(0, 2, 3, 4, 1))
+    # bf16 maps into an f32 channels-last volume at 10 views: written in f32 by the kernel
+    # (no bf16 round trip), bit-identical to the NCDHW f32 volume of the same bf16 maps
+    fb = feat.to(torch.bfloat16)
+    cl32 = v2v.unproject_channels_last(fb, P, coords, "softmax", out_dtype=torch.float32)
+    ref32 = op.unproject_heatmaps(fb, P, coords, "softmax", out_dtype=torch.float32)
+    assert cl32.dtype == torch.float32 and torch.equal(cl32, ref32.permute(0, 2, 3, 4, 1))
     empty = v2v.unproject_channels_last(feat[:0], P[:0], coords[:0], "softmax")
     assert empty.shape == (0, 16, 16, 16, 32) and empty.dtype == torch.bfloat16
     g = torch.Generator().manual_seed(0)

@@ -37,3 +37,23 @@ def test_eager_call_on_cpu_tensors_fails_loudly():
     from mvn_rocm import op
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         op.unproject_heatmaps(torch.randn(1, 4, 4, 8, 8), torch.randn(1, 4, 3, 4), torch.randn(1, 4, 4, 4, 3))
+
+
+def test_tracers_and_transforms_route_through_the_dispatcher():
+    """_ops.call takes the eager bypass only when nothing records or transforms the call:
+    torch.jit.trace and functorch transforms (vmap) must see the registered ops."""
+    from mvn_rocm import _ops
+    seen = []
+
+    def f(x):
+        seen.append(_ops._tracing())
+        return x + 1
+
+    f(torch.randn(2))
+    assert seen == [False]
+    seen.clear()
+    torch.jit.trace(f, torch.randn(2), check_trace=False)
+    assert seen and all(seen), seen
+    seen.clear()
+    torch.func.vmap(f)(torch.randn(3, 2))
+    assert seen == [True], seen

@@ -253,13 +253,17 @@ int mvn_unproject_backward(const void* feat, int feat_dtype, const float* proj, 
 
 /*
  * Deterministic variant of mvn_unproject_backward (the reference trains under
- * autograd.detect_anomaly, train.py:178) and mvn_rocm's default backward: every contribution
- * is scaled by a per-call power of two 2^e and accumulated as a 64-bit integer (integer adds
- * are associative), then converted to f32 — two runs are bit-identical.  e is derived on the
- * device from max |grad_out|, |feat| and |conf| so that no sum can overflow; the integer
- * sums are then exact and the result is the f32 rounding of the exact sum.  Any non-finite
- * grad_out / feat / conf value makes every output NaN.  ~4x faster than the float-atomic
- * variant at config 2.
+ * autograd.detect_anomaly, train.py:178) and mvn_rocm's default backward: every finite
+ * contribution is scaled by a power of two 2^e and accumulated as a 64-bit integer (integer
+ * adds are associative), then converted to f32 — two runs are bit-identical.  e is chosen per
+ * (frame, channel) plane on the device from that plane's finite maxima of |grad_out| (and
+ * |feat| for softmax, |conf| and |feat| for conf*) so that no sum of the plane can overflow;
+ * an element whose exact sum is above 2^-38 of the plane's bound nvox * max|g| * factor comes
+ * out as the f32 rounding of that exact sum (below, its absolute error is at most 2^-62 of
+ * the bound).  Non-finite contributions follow the reference's autograd element by element: a
+ * NaN / inf grad_out, feature or confidence reaches exactly the gradient elements it reaches
+ * in ATen's grid_sampler / softmax / mul backward (NaN if a NaN or both infinities meet there,
+ * else the infinity); every other element stays finite.
  *   workspace  >= mvn_unproject_backward_workspace_bytes(B, N, C, H, W) bytes, any content
  *   grad_feat / grad_conf are fully written (no zero-initialisation needed).
  */

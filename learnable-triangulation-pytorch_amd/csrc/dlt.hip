@@ -196,8 +196,25 @@ __global__ __launch_bounds__(kDltBlock) void dlt_kernel(const float* __restrict_
     }
   }
 
+  // An exactly zero column k of A (all-zero confidences, a coordinate no camera sees) leaves
+  // R's column k exactly zero (the rotations mix rows, never columns), and e_k is an exact null
+  // vector; LAPACK's SVD returns it as V[:, 3], the last of the tied smallest singular values
+  // when there are several (A = 0: V = I, so e_4 and the point (0, 0, 0)).  The reference's
+  // X[:3] / X[3] then gives (0, 0, 0) for k = 3 and (nan, nan, +-inf) otherwise
+  // (multiview.py:154-157); iterating on the singular R would return ratios of tiny numbers.
+  int zcol = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    bool z = true;
+#pragma unroll
+    for (int i = 0; i <= k; ++i) z &= R[i][k] == 0.0;
+    if (z) zcol = k;
+  }
   double X[4];
-  if (!inverse_iteration(R, X)) {
+  if (zcol >= 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) X[i] = i == zcol ? 1.0 : 0.0;
+  } else if (!inverse_iteration(R, X)) {
     double V[4][4];
     jacobi_svd(R, V);
     int kmin = 0;
@@ -205,7 +222,7 @@ __global__ __launch_bounds__(kDltBlock) void dlt_kernel(const float* __restrict_
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const double n2 = R[0][k] * R[0][k] + R[1][k] * R[1][k] + R[2][k] * R[2][k] + R[3][k] * R[3][k];
-      if (k == 0 || n2 < smin) { smin = n2; kmin = k; }
+      if (k == 0 || n2 <= smin) { smin = n2; kmin = k; }     // ties: the last, as LAPACK's order
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

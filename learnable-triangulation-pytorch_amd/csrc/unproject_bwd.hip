@@ -20,14 +20,22 @@
 // last bits (documented in DESIGN.md).
 //
 // Fixed-point mode (DET; mvn_unproject_backward_deterministic — the Python layer's default):
-// every contribution — the same f32 product as above — is scaled by a per-call power of two
-// 2^e and rounded to a 64-bit integer; the LDS and the global accumulation are integer adds
+// every finite contribution — the same f32 product as above — is scaled by a power of two 2^e
+// and rounded to a 64-bit integer; the LDS and the global accumulation are integer adds
 // (ds_add_u64 / global_atomic_add_x2), which are associative, so the sums do not depend on
-// the order the waves and blocks arrive in and two runs are bit-identical.  e comes from
-// the inputs' magnitudes on the device (absmax_bits, fix_scale: no host sync) so that no sum
-// can overflow; at that scale the contributions convert exactly, the integer sums are exact
-// and the last kernel's conversion gives the f32 rounding of the exact sum (a float-atomic
-// sum rounds at every add).  A non-finite input makes every gradient NaN.
+// the order the waves and blocks arrive in and two runs are bit-identical.  e is chosen per
+// (frame, channel) plane — every element of grad_feat[b, :, c] and grad_conf[b, :, c] shares
+// it — on the device (fix_scale_planes: no host sync) from that plane's finite maxima, so
+// that no sum of the plane can leave +-2^62.  Range: the unit is 2^-62 of the plane's bound
+// nvox * max|g| * factor, so an element keeps all 24 bits when its exact sum is above
+// 2^-38 of that bound (2^-20 of max|g| * factor at 64^3) and is then the f32 rounding of the
+// exact sum; below, its absolute error is at most the unit (a frame or channel whose gradients
+// are 1e8 x smaller than another's has its own scale).
+// Non-finite contributions (a NaN or infinite grad_out / feature / confidence reaching a tap)
+// are not summed: they set per-element flags (NaN, +inf, -inf) with atomicOr, and the element
+// comes out as the reference's sequential float sum would: NaN if a NaN or both infinities
+// reached it, else the infinity.  Elements no non-finite contribution reaches stay finite —
+// ATen's grid_sampler backward confines a NaN to the taps it touches.
 #include <algorithm>
 
 #include "unproject_common.hpp"
@@ -45,43 +53,62 @@ constexpr int TX = 4, TY = 8, TZ = 8;        // one voxel per thread
 
 template <typename T> __device__ __forceinline__ float ldf(const T* p, size_t i) { return to_f32(p[i]); }
 
-// Fixed-point mode (DET): an f32 contribution x becomes round(x * 2^e) in a 64-bit integer.
-// e is chosen per call on the device (fix_scale) from the inputs' magnitudes so that no sum
-// can leave +-2^62: |every accumulated sum| <= nvox * max|g| * max(1, max|conf|) *
-// (1 + 2 max|feat|) (bilinear weights of a voxel-view sum to <= 1; |d agg / d s| <= 1 + 2
-// max|s| for softmax, conf for conf*).  Typical contributions are then >= 2^24 units, so
-// the scaling and the integer conversion are exact and the integer sums are exact: the
-// result is the f32 rounding of the exact sum, in any arrival order.  (Clamp: guard only.)
+// Fixed-point mode (DET): a finite f32 contribution x becomes round(x * 2^e) in a 64-bit integer
+// (e of the element's (frame, channel) plane, so that no sum can leave +-2^62; clamp: guard only).
 __device__ __forceinline__ unsigned long long to_fix(float x, float scale) {
   const float y = fminf(fmaxf(x * scale, -0x1p62f), 0x1p62f);
   return static_cast<unsigned long long>(__float2ll_rn(y));
 }
-// per-call header at the start of the fixed-point workspace
-struct FixHeader {
-  unsigned gbits, fbits, cbits, pad;   // max |grad_out|, |feat|, |conf| as f32 bits (NaN above inf)
-  float scale;                         // 2^e
-  int valid;                           // 0: a non-finite input; the gradients are NaN
-  double inv;                          // 2^-e
+// non-finite contribution flags (per element, atomicOr): the reference's float sum of them
+constexpr unsigned kFlagNaN = 1u, kFlagPinf = 2u, kFlagNinf = 4u;
+__device__ __forceinline__ unsigned nonfinite_flag(float x) {
+  return x != x ? kFlagNaN : (x > 0.f ? kFlagPinf : kFlagNinf);
+}
+// the workspace: a 256-byte header, the per-(frame, channel) scales 2^e as f32 and 2^-e as f64,
+// then a 64-bit word and a 32-bit flag word per feature element and confidence
+constexpr size_t kFixHeaderBytes = 256;
+// the fixed-point outputs of a call (DET)
+struct FixArgs {
+  unsigned long long* qfeat;   // per feature element
+  unsigned long long* qconf;   // per confidence (conf* with grad_conf)
+  unsigned* ffeat;             // non-finite flags per feature element
+  unsigned* fconf;             // non-finite flags per confidence
+  const float* scale;          // 2^e per (frame, channel)
 };
-// header, then per-block partial maxima of |grad_out|, |feat|, |conf| (kMaxParts each): the
-// maxima are reduced in two levels without atomics (thousands of same-address atomics
-// serialise at the memory side)
-constexpr int kMaxParts = 1024;
-constexpr size_t kFixPartsOffset = 256;
-constexpr size_t kFixHeaderBytes = kFixPartsOffset + 3 * kMaxParts * sizeof(unsigned);
-// float accumulate (default) or fixed-point accumulate (DET) into a global element
+// one contribution into global memory: float atomics (default) or the fixed point + flags (DET)
 template <bool DET>
-__device__ __forceinline__ void global_add(float* f, unsigned long long* q, size_t i, float x, float scale) {
-  if constexpr (DET) atomicAdd(q + i, to_fix(x, scale));
-  else atomicAdd(f + i, x);
+__device__ __forceinline__ void global_add(float* f, unsigned long long* q, unsigned* fl, size_t i, float x,
+                                           float scale) {
+  if constexpr (DET) {
+    if (__builtin_isfinite(x)) atomicAdd(q + i, to_fix(x, scale));
+    else atomicOr(fl + i, nonfinite_flag(x));
+  } else {
+    atomicAdd(f + i, x);
+  }
+}
+// a fixed-point sum q (scaled by 2^e) -> the f32 rounding of its value: the top 53 bits of |q|
+// with the rest folded into the last bit (round to odd), exact in f64, then one f64 -> f32
+// rounding (53 >= 24 + 2: correct, f32 subnormals included; a plain double(q) would round twice)
+__device__ __forceinline__ float fix_to_float(unsigned long long q, int e) {
+  const bool neg = static_cast<long long>(q) < 0;
+  const unsigned long long m = neg ? ~q + 1ull : q;
+  if (m == 0ull) return 0.f;                           // +0, as a float sum of x and -x
+  const int lz = __clzll(static_cast<long long>(m));
+  const unsigned long long top = m << lz;
+  const unsigned long long t53 = (top >> 11) | ((top & 0x7ffull) != 0ull ? 1ull : 0ull);
+  const float f = static_cast<float>(ldexp(static_cast<double>(t53), 63 - lz - 52 - e));
+  return neg ? -f : f;
+}
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long x, int o) {
+  const int lo = __shfl_xor(int(unsigned(x)), o, kWave), hi = __shfl_xor(int(unsigned(x >> 32)), o, kWave);
+  return (static_cast<unsigned long long>(unsigned(hi)) << 32) | unsigned(lo);
 }
 
 template <int AGG, typename TIn, typename TG, int NV, bool DET>
 __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ conf, const TG* __restrict__ gout, float* __restrict__ gfeat,
-    float* __restrict__ gconf, unsigned long long* __restrict__ qfeat, unsigned long long* __restrict__ qconf,
-    const float* __restrict__ fixscale, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners) {
+    float* __restrict__ gconf, FixArgs fa, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int align_corners) {
   constexpr bool kNeedSamples = AGG == MVN_AGG_SOFTMAX || AGG == MVN_AGG_MAX || AGG == MVN_AGG_CONF;
   __shared__ float4 fstage[kSlots];          // forward features (channels-last)
   __shared__ float4 gacc[DET ? 1 : kSlots];  // gradient accumulator (channels-last)
@@ -91,8 +118,6 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
   __shared__ float gconf_acc[NV][G];
   __shared__ unsigned long long gconf_q[DET ? NV : 1][G];
   __shared__ int info[2];                    // total slots (or -1: direct global path)
-  float fsc = 0.f;                           // 2^e of this call (DET)
-  if constexpr (DET) fsc = *fixscale;
 
   const int nTx = (Vx + TX - 1) / TX, nTy = (Vy + TY - 1) / TY, nTz = (Vz + TZ - 1) / TZ;
   int L = xcd_remap(blockIdx.x, B * nTx * nTy * nTz);
@@ -198,15 +223,23 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
         else if constexpr (AGG == MVN_AGG_CONF) coef[v] = g * conf[(size_t(b) * N + v) * C + c];
         else if constexpr (AGG == MVN_AGG_MAX) coef[v] = v == arg ? g : 0.f;
         else coef[v] = g * (softmax_exp(s[v], m * kLog2e) * __builtin_amdgcn_rcpf(den)) * (1.f + s[v] - out);
+        const float fsc = DET ? fa.scale[size_t(b) * C + c] : 0.f;
         if (coef[v] != 0.f) {
+          // every in-image tap of the voxel-view receives coef * w (ATen grid_sampler backward:
+          // a zero weight still carries a NaN or infinite coefficient as NaN)
           const size_t pl = fbo + (size_t(v) * C + c) * HW;
-          if (tp[v].w0 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o0, coef[v] * tp[v].w0, fsc);
-          if (tp[v].w1 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o1, coef[v] * tp[v].w1, fsc);
-          if (tp[v].w2 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o2, coef[v] * tp[v].w2, fsc);
-          if (tp[v].w3 != 0.f) global_add<DET>(gfeat, qfeat, pl + tp[v].o3, coef[v] * tp[v].w3, fsc);
+          const int o[4] = {tp[v].o0, tp[v].o1, tp[v].o2, tp[v].o3};
+          const float wt[4] = {tp[v].w0, tp[v].w1, tp[v].w2, tp[v].w3};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float x = coef[v] * wt[q];
+            if (((tp[v].in >> q) & 1u) && x != 0.f) global_add<DET>(gfeat, fa.qfeat, fa.ffeat, pl + o[q], x, fsc);
+          }
         }
+        // (an invalid voxel-view's sample is the masked 0: g * 0, NaN only for a NaN / inf g)
         if constexpr (AGG == MVN_AGG_CONF)
-          if (gconf && v < N && g * s[v] != 0.f) global_add<DET>(gconf, qconf, (size_t(b) * N + v) * C + c, g * s[v], fsc);
+          if (gconf && v < N && g * s[v] != 0.f)
+            global_add<DET>(gconf, fa.qconf, fa.fconf, (size_t(b) * N + v) * C + c, g * s[v], fsc);
       }
     }
     return;
@@ -259,9 +292,12 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
     __syncthreads();
 
     // ---- per voxel: samples, upstream gradient, d agg / d s_v, LDS scatter ------------
-    float g[G];
+    float g[G], fsc[G];
 #pragma unroll
-    for (int k = 0; k < G; ++k) g[k] = (act && c0 + k < C) ? ldf(gb, size_t(c0 + k) * nvox) : 0.f;
+    for (int k = 0; k < G; ++k) {
+      g[k] = (act && c0 + k < C) ? ldf(gb, size_t(c0 + k) * nvox) : 0.f;
+      fsc[k] = (DET && c0 + k < C) ? fa.scale[size_t(b) * C + c0 + k] : 0.f;   // 2^e of the plane
+    }
     float s[NV][G];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -312,12 +348,24 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
       for (int v = 0; v < NV; ++v) {
         if (v >= N || !has[v] || coef[v] == 0.f) continue;
         if constexpr (DET) {
-          unsigned long long* q0 = &gq[slot[v] * G + k];
-          unsigned long long* q1 = &gq[(slot[v] + rpitch[v]) * G + k];
-          atomicAdd(q0, to_fix(coef[v] * w[v][0], fsc));
-          atomicAdd(q0 + G, to_fix(coef[v] * w[v][1], fsc));
-          atomicAdd(q1, to_fix(coef[v] * w[v][2], fsc));
-          atomicAdd(q1 + G, to_fix(coef[v] * w[v][3], fsc));
+          // the weights are finite and at most 1, so coef * w is non-finite exactly when coef
+          // is: that rare case (a NaN or infinite input) flags the in-image taps directly
+          if (__builtin_isfinite(coef[v])) {
+            unsigned long long* q0 = &gq[slot[v] * G + k];
+            unsigned long long* q1 = &gq[(slot[v] + rpitch[v]) * G + k];
+            atomicAdd(q0, to_fix(coef[v] * w[v][0], fsc[k]));
+            atomicAdd(q0 + G, to_fix(coef[v] * w[v][1], fsc[k]));
+            atomicAdd(q1, to_fix(coef[v] * w[v][2], fsc[k]));
+            atomicAdd(q1 + G, to_fix(coef[v] * w[v][3], fsc[k]));
+          } else {
+#pragma unroll 1
+            for (int q = 0; q < 4; ++q) {
+              const int gx = fx[v] + (q & 1), gy = fy[v] + (q >> 1);
+              if (gx >= 0 && gx < W && gy >= 0 && gy < H && c < C)
+                atomicOr(fa.ffeat + fbo + (size_t(v) * C + c) * HW + size_t(gy) * W + gx,
+                         nonfinite_flag(coef[v] * w[v][q]));
+            }
+          }
         } else {
           float* base0 = reinterpret_cast<float*>(&gacc[slot[v]]) + k;
           float* base1 = reinterpret_cast<float*>(&gacc[slot[v] + rpitch[v]]) + k;
@@ -332,12 +380,21 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
 #pragma unroll
           for (int v = 0; v < NV; ++v) {
             if (v >= N) continue;
+            // (an invalid voxel-view's sample is the masked 0, op.py:137: g * 0 carries only a
+            // NaN / infinite g; g is 0 past the tile and C)
             float part = g[k] * s[v][k];
+            if constexpr (DET) {
+              // exact: each lane's term in fixed point, summed by integer butterflies
+              unsigned long long q = 0ull;
+              if (__builtin_isfinite(part)) q = to_fix(part, fsc[k]);
+              else atomicOr(fa.fconf + (size_t(b) * N + v) * C + c, nonfinite_flag(part));
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
-            if (lane == 0 && part != 0.f) {
-              if constexpr (DET) atomicAdd(&gconf_q[v][k], to_fix(part, fsc));
-              else atomicAdd(&gconf_acc[v][k], part);
+              for (int o = 32; o > 0; o >>= 1) q += shfl_xor_u64(q, o);
+              if (lane == 0 && q != 0ull) atomicAdd(&gconf_q[v][k], q);
+            } else {
+#pragma unroll
+              for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
+              if (lane == 0 && part != 0.f) atomicAdd(&gconf_acc[v][k], part);
             }
           }
         }
@@ -361,7 +418,7 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
 #pragma unroll
           for (int k = 0; k < G; ++k) {
             const unsigned long long q = gq[idx * G + k];
-            if (c0 + k < C && q != 0ull) atomicAdd(qfeat + pix + (size_t(v) * C + c0 + k) * HW, q);
+            if (c0 + k < C && q != 0ull) atomicAdd(fa.qfeat + pix + (size_t(v) * C + c0 + k) * HW, q);
           }
         } else {
           const float4 a = gacc[idx];
@@ -377,7 +434,7 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
         const int v = t / G, k = t % G;
         const size_t o = (size_t(b) * N + v) * C + c0 + k;
         if constexpr (DET) {
-          if (v < N && c0 + k < C && gconf_q[v][k] != 0ull) atomicAdd(qconf + o, gconf_q[v][k]);
+          if (v < N && c0 + k < C && gconf_q[v][k] != 0ull) atomicAdd(fa.qconf + o, gconf_q[v][k]);
         } else {
           if (v < N && c0 + k < C && gconf_acc[v][k] != 0.f) atomicAdd(gconf + o, gconf_acc[v][k]);
         }
@@ -387,74 +444,92 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
   }
 }
 
-// max |x| of a tensor as f32 bits (|x| >= 0 orders like its bits; NaN's bits sort above inf):
-// one partial per block into part[blockIdx.x] (gridDim.x <= kMaxParts)
+// max |x| over the finite values among n elements at x[i * stride .. + len) (several strided
+// runs: the views of a (frame, channel) plane), as f32 bits (|x| >= 0 orders like its bits), one
+// 256-thread block
 template <typename T>
-__global__ __launch_bounds__(256) void absmax_bits(const T* __restrict__ x, size_t n, unsigned* __restrict__ part) {
-  __shared__ unsigned wmax[256 / kWave];
+__device__ __forceinline__ unsigned block_absmax(const T* __restrict__ x, int runs, size_t stride, size_t len,
+                                                 unsigned* red) {
   unsigned m = 0;
-  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-    m = max(m, __float_as_uint(fabsf(to_f32(x[i]))));
+  for (int r = 0; r < runs; ++r)
+    for (size_t i = threadIdx.x; i < len; i += blockDim.x) {
+      const unsigned bits = __float_as_uint(fabsf(to_f32(x[r * stride + i])));
+      m = max(m, bits < 0x7f800000u ? bits : 0u);        // non-finite values are flagged, not summed
+    }
 #pragma unroll
   for (int o = kWave / 2; o > 0; o >>= 1) m = max(m, unsigned(__shfl_xor(int(m), o, kWave)));
-  if ((threadIdx.x & (kWave - 1)) == 0) wmax[threadIdx.x / kWave] = m;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned b = 0;
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = m;
+  __syncthreads();
+  unsigned b = 0;
 #pragma unroll
-    for (int w = 0; w < 256 / kWave; ++w) b = max(b, wmax[w]);
-    part[blockIdx.x] = b;
-  }
+  for (int w = 0; w < 256 / kWave; ++w) b = max(b, red[w]);
+  return b;
 }
-// the call's fixed-point exponent from the partial maxima (one block of 256 threads)
-__global__ __launch_bounds__(256) void fix_scale(FixHeader* __restrict__ h, const unsigned* __restrict__ parts,
-                                                 double nvox) {
-  __shared__ unsigned red[3][256 / kWave];
-  unsigned m[3] = {0u, 0u, 0u};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    for (int i = threadIdx.x; i < kMaxParts; i += 256) m[k] = max(m[k], parts[k * kMaxParts + i]);
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) m[k] = max(m[k], unsigned(__shfl_xor(int(m[k]), o, kWave)));
-    if ((threadIdx.x & (kWave - 1)) == 0) red[k][threadIdx.x / kWave] = m[k];
+// the fixed-point scale 2^e of each (frame, channel) plane, one block per plane.  Bound on any
+// sum of the plane (finite contributions only; a voxel-view's bilinear weights sum to <= 1, so
+// each voxel adds at most |coefficient| to an element): nvox * max|g| * factor, factor = 1
+// (sum, max), max(1, max|conf|) for the feature and max|feat| for the confidence gradient
+// (conf*), 1 + 2 max|feat| (softmax: |d agg / d s_v| <= 1 + 2 max|s|).  e puts it below 2^62.
+template <typename TIn, typename TG>
+__global__ __launch_bounds__(256) void fix_scale_planes(const TIn* __restrict__ feat, const TG* __restrict__ gout,
+                                                        const float* __restrict__ conf, float* __restrict__ scale,
+                                                        int* __restrict__ expo, int N, int C, int HW, int nvox,
+                                                        int agg) {
+  __shared__ unsigned red[256 / kWave];
+  const int b = blockIdx.x / C, c = blockIdx.x % C;
+  const double g = __uint_as_float(block_absmax(gout + (size_t(b) * C + c) * nvox, 1, 0, size_t(nvox), red));
+  double factor = 1.0;
+  if (agg == MVN_AGG_SOFTMAX || agg == MVN_AGG_CONF) {
+    const double f = __uint_as_float(
+        block_absmax(feat + (size_t(b) * N * C + c) * HW, N, size_t(C) * HW, size_t(HW), red));
+    if (agg == MVN_AGG_SOFTMAX) {
+      factor = 1.0 + 2.0 * f;
+    } else {
+      unsigned cm = 0;
+      for (int v = 0; v < N; ++v) {
+        const unsigned bits = __float_as_uint(fabsf(conf[(size_t(b) * N + v) * C + c]));
+        cm = max(cm, bits < 0x7f800000u ? bits : 0u);
+      }
+      factor = fmax(fmax(1.0, double(__uint_as_float(cm))), f);
+    }
   }
-  __syncthreads();
   if (threadIdx.x != 0) return;
-  unsigned gb = 0, fb = 0, cb = 0;
-#pragma unroll
-  for (int w = 0; w < 256 / kWave; ++w) { gb = max(gb, red[0][w]); fb = max(fb, red[1][w]); cb = max(cb, red[2][w]); }
-  const bool finite = gb < 0x7f800000u && fb < 0x7f800000u && cb < 0x7f800000u;
-  const double g = __uint_as_float(gb), f = __uint_as_float(fb), c = __uint_as_float(cb);
-  const double bound = nvox * g * fmax(1.0, c) * (1.0 + 2.0 * f);
+  const double bound = double(nvox) * g * factor;
   int e = 62;
-  if (finite && bound > 0.0) e = int(floor(62.0 - log2(bound))) - 1;
+  if (bound > 0.0) e = int(floor(62.0 - log2(bound))) - 1;
   e = min(max(e, -120), 120);
-  h->gbits = gb; h->fbits = fb; h->cbits = cb;
-  h->scale = ldexpf(1.f, e);
-  h->inv = ldexp(1.0, -e);
-  h->valid = finite ? 1 : 0;
+  scale[blockIdx.x] = ldexpf(1.f, e);
+  expo[blockIdx.x] = e;
 }
-// fixed-point sums (DET) -> f32 gradients
-__global__ void fix_to_f32(const unsigned long long* __restrict__ q, float* __restrict__ out, size_t n,
-                           const FixHeader* __restrict__ h) {
-  const double inv = h->inv;
-  const bool valid = h->valid != 0;
-  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-    out[i] = valid ? float(double(static_cast<long long>(q[i])) * inv) : __builtin_nanf("");
+// fixed-point sums + non-finite flags (DET) -> f32 gradients; element i belongs to the plane
+// (i / per_b) * C + (i / per_c) % C (per_c elements per channel run, per_b per frame)
+__global__ void fix_to_f32(const unsigned long long* __restrict__ q, const unsigned* __restrict__ flags,
+                           float* __restrict__ out, size_t n, const int* __restrict__ expo, int C, size_t per_c,
+                           size_t per_b) {
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+    const size_t plane = (i / per_b) * C + (i / per_c) % C;
+    const unsigned f = flags[i];
+    float r = fix_to_float(q[i], expo[plane]);
+    if (f) r = ((f & kFlagNaN) || (f & (kFlagPinf | kFlagNinf)) == (kFlagPinf | kFlagNinf))
+                   ? __builtin_nanf("")
+                   : (f & kFlagPinf ? __builtin_inff() : -__builtin_inff());
+    out[i] = r;
+  }
 }
 
 template <int AGG, typename TIn, typename TG, bool DET>
 int launch_bwd(const void* feat, const float* P, const float* coords, const float* conf, const void* gout, float* gfeat,
-               float* gconf, unsigned long long* qfeat, unsigned long long* qconf, const float* fixs, int B, int N,
+               float* gconf, FixArgs fa, int B, int N,
                int C, int H, int W, int Vx, int Vy, int Vz, int ac, hipStream_t s) {
   const long long nb = (long long)B * ((Vx + TX - 1) / TX) * ((Vy + TY - 1) / TY) * ((Vz + TZ - 1) / TZ);
   if (nb > INT_MAX) return MVN_ERR_SHAPE;
   if (N <= 4)
     unproject_bwd_tiled<AGG, TIn, TG, 4, DET><<<int(nb), kThreads, 0, s>>>(static_cast<const TIn*>(feat), P, coords,
-        conf, static_cast<const TG*>(gout), gfeat, gconf, qfeat, qconf, fixs, B, N, C, H, W, Vx, Vy, Vz, ac);
+        conf, static_cast<const TG*>(gout), gfeat, gconf, fa, B, N, C, H, W, Vx, Vy, Vz, ac);
   else if (N <= 8)
     unproject_bwd_tiled<AGG, TIn, TG, 8, DET><<<int(nb), kThreads, 0, s>>>(static_cast<const TIn*>(feat), P, coords,
-        conf, static_cast<const TG*>(gout), gfeat, gconf, qfeat, qconf, fixs, B, N, C, H, W, Vx, Vy, Vz, ac);
+        conf, static_cast<const TG*>(gout), gfeat, gconf, fa, B, N, C, H, W, Vx, Vy, Vz, ac);
   else
     return MVN_ERR_SHAPE;
   return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
@@ -462,20 +537,20 @@ int launch_bwd(const void* feat, const float* P, const float* coords, const floa
 
 template <typename TIn, typename TG, bool DET>
 int dispatch_bwd(int agg, const void* feat, const float* P, const float* coords, const float* conf, const void* gout,
-                 float* gfeat, float* gconf, unsigned long long* qfeat, unsigned long long* qconf, const float* fixs,
+                 float* gfeat, float* gconf, FixArgs fa,
                  int B, int N, int C, int H, int W, int Vx, int Vy, int Vz, int ac, hipStream_t s) {
   switch (agg) {
     case MVN_AGG_SUM:
-      return launch_bwd<MVN_AGG_SUM, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, fixs, B, N, C, H,
+      return launch_bwd<MVN_AGG_SUM, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, fa, B, N, C, H,
                                                    W, Vx, Vy, Vz, ac, s);
     case MVN_AGG_MAX:
-      return launch_bwd<MVN_AGG_MAX, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, fixs, B, N, C, H,
+      return launch_bwd<MVN_AGG_MAX, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, fa, B, N, C, H,
                                                    W, Vx, Vy, Vz, ac, s);
     case MVN_AGG_SOFTMAX:
-      return launch_bwd<MVN_AGG_SOFTMAX, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, fixs, B, N,
+      return launch_bwd<MVN_AGG_SOFTMAX, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, fa, B, N,
                                                        C, H, W, Vx, Vy, Vz, ac, s);
     case MVN_AGG_CONF:
-      return launch_bwd<MVN_AGG_CONF, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, qfeat, qconf, fixs, B, N, C,
+      return launch_bwd<MVN_AGG_CONF, TIn, TG, DET>(feat, P, coords, conf, gout, gfeat, gconf, fa, B, N, C,
                                                     H, W, Vx, Vy, Vz, ac, s);
   }
   return MVN_ERR_ARG;
@@ -484,20 +559,18 @@ int dispatch_bwd(int agg, const void* feat, const float* P, const float* coords,
 template <bool DET>
 int backward_entry(const void* feat, int feat_dtype, const float* proj, const float* coords, const float* conf,
                    const void* grad_out, int grad_out_dtype, float* grad_feat, float* grad_conf,
-                   unsigned long long* qfeat, unsigned long long* qconf, const float* fixs, int B, int N, int C, int H,
+                   FixArgs fa, int B, int N, int C, int H,
                    int W, int Vx, int Vy, int Vz, int agg, int align_corners, hipStream_t s) {
   const bool f16 = feat_dtype == MVN_DTYPE_BF16, g16 = grad_out_dtype == MVN_DTYPE_BF16;
   if ((feat_dtype != MVN_DTYPE_F32 && !f16) || (grad_out_dtype != MVN_DTYPE_F32 && !g16)) return MVN_ERR_DTYPE;
   if (!f16 && !g16)
-    return dispatch_bwd<float, float, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat, qconf, fixs,
+    return dispatch_bwd<float, float, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, fa,
                                            B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
   if (f16 && g16)
-    return dispatch_bwd<uint16_t, uint16_t, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat,
-                                                 qconf, fixs, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+    return dispatch_bwd<uint16_t, uint16_t, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, fa, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
   if (f16)
-    return dispatch_bwd<uint16_t, float, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat,
-                                              qconf, fixs, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
-  return dispatch_bwd<float, uint16_t, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, qfeat, qconf, fixs,
+    return dispatch_bwd<uint16_t, float, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, fa, B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
+  return dispatch_bwd<float, uint16_t, DET>(agg, feat, proj, coords, conf, grad_out, grad_feat, grad_conf, fa,
                                             B, N, C, H, W, Vx, Vy, Vz, align_corners, s);
 }
 
@@ -527,13 +600,17 @@ extern "C" int mvn_unproject_backward(const void* feat, int feat_dtype, const fl
                                align_corners);
   if (e != MVN_OK) return e;
   return backward_entry<false>(feat, feat_dtype, proj, coords, conf, grad_out, grad_out_dtype, grad_feat, grad_conf,
-                               nullptr, nullptr, nullptr, B, N, C, H, W, Vx, Vy, Vz, agg, align_corners,
+                               FixArgs{}, B, N, C, H, W, Vx, Vy, Vz, agg, align_corners,
                                static_cast<hipStream_t>(stream));
 }
 
 extern "C" size_t mvn_unproject_backward_workspace_bytes(int B, int N, int C, int H, int W) {
   if (B <= 0 || N <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
-  return mvn::unproj::kFixHeaderBytes + (size_t(B) * N * C * size_t(H) * W + size_t(B) * N * C) * sizeof(unsigned long long);
+  // header, 2^e (f32) and e (int) per (frame, channel), then a 64-bit word and a 32-bit flag per
+  // feature element and confidence
+  const size_t planes = size_t(B) * C;
+  return mvn::unproj::kFixHeaderBytes + ((planes * 8 + 255) / 256) * 256 +
+         (size_t(B) * N * C * size_t(H) * W + size_t(B) * N * C) * (sizeof(unsigned long long) + sizeof(unsigned));
 }
 
 extern "C" int mvn_unproject_backward_deterministic(const void* feat, int feat_dtype, const float* proj,
@@ -550,31 +627,40 @@ extern "C" int mvn_unproject_backward_deterministic(const void* feat, int feat_d
   const size_t nfeat = size_t(B) * N * C * size_t(H) * W, nconf = size_t(B) * N * C;
   if (!workspace || workspace_bytes < mvn_unproject_backward_workspace_bytes(B, N, C, H, W)) return MVN_ERR_WORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  auto* hdr = static_cast<FixHeader*>(workspace);
-  auto* qfeat = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + kFixHeaderBytes);
+  const size_t planes = size_t(B) * C;
+  char* ws = static_cast<char*>(workspace);
+  auto* scale = reinterpret_cast<float*>(ws + kFixHeaderBytes);
+  auto* expo = reinterpret_cast<int*>(scale + planes);
+  auto* qfeat = reinterpret_cast<unsigned long long*>(ws + kFixHeaderBytes + ((planes * 8 + 255) / 256) * 256);
   auto* qconf = qfeat + nfeat;
-  if (hipMemsetAsync(workspace, 0, kFixHeaderBytes + (nfeat + nconf) * sizeof(unsigned long long), s) != hipSuccess)
+  auto* ffeat = reinterpret_cast<unsigned*>(qconf + nconf);
+  auto* fconf = ffeat + nfeat;
+  if (hipMemsetAsync(qfeat, 0, (nfeat + nconf) * (sizeof(unsigned long long) + sizeof(unsigned)), s) != hipSuccess)
     return MVN_ERR_LAUNCH;
-  // the call's fixed-point scale from max |grad_out|, |feat|, |conf| (device-side: no sync)
-  auto* parts = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + kFixPartsOffset);
-  const size_t ngrad = size_t(B) * C * size_t(Vx) * Vy * Vz;
-  auto nblk_of = [](size_t n) { return int(std::min<size_t>((n + 255) / 256, kMaxParts)); };
-  if (grad_out_dtype == MVN_DTYPE_BF16)
-    absmax_bits<<<nblk_of(ngrad), 256, 0, s>>>(static_cast<const uint16_t*>(grad_out), ngrad, parts);
+  // the fixed-point scale of each (frame, channel) plane from its finite maxima (device-side)
+  if (planes > INT_MAX) return MVN_ERR_SHAPE;
+  const int nvox = Vx * Vy * Vz, HW = H * W;
+  const bool f16 = feat_dtype == MVN_DTYPE_BF16, g16 = grad_out_dtype == MVN_DTYPE_BF16;
+  if ((feat_dtype != MVN_DTYPE_F32 && !f16) || (grad_out_dtype != MVN_DTYPE_F32 && !g16)) return MVN_ERR_DTYPE;
+  const int nb = int(planes);
+  if (f16 && g16)
+    fix_scale_planes<<<nb, 256, 0, s>>>(static_cast<const uint16_t*>(feat), static_cast<const uint16_t*>(grad_out), conf,
+                                        scale, expo, N, C, HW, nvox, agg);
+  else if (f16)
+    fix_scale_planes<<<nb, 256, 0, s>>>(static_cast<const uint16_t*>(feat), static_cast<const float*>(grad_out), conf,
+                                        scale, expo, N, C, HW, nvox, agg);
+  else if (g16)
+    fix_scale_planes<<<nb, 256, 0, s>>>(static_cast<const float*>(feat), static_cast<const uint16_t*>(grad_out), conf,
+                                        scale, expo, N, C, HW, nvox, agg);
   else
-    absmax_bits<<<nblk_of(ngrad), 256, 0, s>>>(static_cast<const float*>(grad_out), ngrad, parts);
-  if (feat_dtype == MVN_DTYPE_BF16)
-    absmax_bits<<<nblk_of(nfeat), 256, 0, s>>>(static_cast<const uint16_t*>(feat), nfeat, parts + kMaxParts);
-  else
-    absmax_bits<<<nblk_of(nfeat), 256, 0, s>>>(static_cast<const float*>(feat), nfeat, parts + kMaxParts);
-  if (agg == MVN_AGG_CONF) absmax_bits<<<nblk_of(nconf), 256, 0, s>>>(conf, nconf, parts + 2 * kMaxParts);
-  fix_scale<<<1, 256, 0, s>>>(hdr, parts, double(Vx) * Vy * Vz);
+    fix_scale_planes<<<nb, 256, 0, s>>>(static_cast<const float*>(feat), static_cast<const float*>(grad_out), conf,
+                                        scale, expo, N, C, HW, nvox, agg);
   const int r = backward_entry<true>(feat, feat_dtype, proj, coords, conf, grad_out, grad_out_dtype, grad_feat,
-                                     grad_conf, qfeat, grad_conf ? qconf : nullptr, &hdr->scale, B, N, C, H, W, Vx,
+                                     grad_conf, FixArgs{qfeat, qconf, ffeat, fconf, scale}, B, N, C, H, W, Vx,
                                      Vy, Vz, agg, align_corners, s);
   if (r != MVN_OK) return r;
   auto cvt_blocks = [](size_t n) { return int(std::min<size_t>((n + 255) / 256, 65536)); };
-  fix_to_f32<<<cvt_blocks(nfeat), 256, 0, s>>>(qfeat, grad_feat, nfeat, hdr);
-  if (grad_conf) fix_to_f32<<<cvt_blocks(nconf), 256, 0, s>>>(qconf, grad_conf, nconf, hdr);
+  fix_to_f32<<<cvt_blocks(nfeat), 256, 0, s>>>(qfeat, ffeat, grad_feat, nfeat, expo, C, size_t(HW), size_t(N) * C * HW);
+  if (grad_conf) fix_to_f32<<<cvt_blocks(nconf), 256, 0, s>>>(qconf, fconf, grad_conf, nconf, expo, C, 1, size_t(N) * C);
   return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
 }

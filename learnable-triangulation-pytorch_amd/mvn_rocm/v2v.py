@@ -71,6 +71,11 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
         raise ValueError("unproject_channels_last: 'conf*' aggregation is not supported here")
     cub = coord_volumes if isinstance(coord_volumes, Cuboids) else None
     feat, proj, _ = unproject_inputs(heatmaps, proj_matricies, None, agg, volume_aggregation_method, cub)
+    if feat.dtype == torch.float32 and out_dtype == torch.bfloat16:
+        # f32 maps into a bf16 volume: the kernels write f32 (no f32 -> bf16 instantiation,
+        # mvn_hip.h), rounded to nearest-even by one device cast
+        return unproject_channels_last(feat, proj, coord_volumes, volume_aggregation_method, torch.float32,
+                                       align_corners).to(torch.bfloat16)
     fd, od = _dtype_code(feat.dtype), _dtype_code(out_dtype)
     B, N, C, H, W = feat.shape
     if N > 8:
@@ -78,7 +83,7 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
         # NCDHW unprojection (any N) and one permute on the device
         from .op import unproject_heatmaps
         # written in out_dtype by the kernel itself (bf16 maps into an f32 volume keep f32
-        # precision; an f32 volume is rounded to bf16 by the kernel's own nearest-even stores)
+        # precision)
         vol = unproject_heatmaps(feat, proj, coord_volumes, volume_aggregation_method, align_corners=align_corners,
                                  out_dtype=out_dtype)
         return vol.permute(0, 2, 3, 4, 1).contiguous()

@@ -2,7 +2,7 @@
 
 Run in the build container only (it needs /root/reference; the GPU box never runs it):
 
-    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes|ce_loss|v2v_front|chains]   (argument: only that fixture)
+    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes|ce_loss|v2v_front|chains|dlt_degenerate]   (argument: only that fixture)
 
 The reference (learnable-triangulation-pytorch, mvn/utils/op.py and
 mvn/utils/multiview.py) is imported read-only with two in-memory accommodations:
@@ -318,6 +318,26 @@ def golden_chains():
     save("chains.npz", **out)
 
 
+def golden_dlt_degenerate(multiview):
+    """Degenerate DLT inputs (SURVEY.md §5 failure row): a joint with all-zero confidences
+    (A = 0) and cameras whose projection ignores z (third column of every P zero, so A has an
+    exactly zero column and X[3] = 0).  The outputs are whatever the reference's torch.svd
+    (LAPACK) returns on THIS host: zeros for A = 0; (nan, nan, +-inf) for the zero column here,
+    while another host's LAPACK may return a non-exact null vector (finite values)."""
+    rng = np.random.default_rng(0)
+    P = torch.from_numpy(rng.normal(size=(2, 4, 3, 4)).astype(np.float32))
+    pts = torch.from_numpy(rng.normal(size=(2, 4, 3, 2)).astype(np.float32))
+    conf = torch.from_numpy(rng.uniform(0.2, 1, (2, 4, 3)).astype(np.float32))
+    conf[0, :, 1] = 0.0
+    conf[1, :, 2] = 0.0
+    out_zero_conf = multiview.triangulate_batch_of_points(P, pts, conf)
+    P2 = P.clone()
+    P2[:, :, :, 2] = 0.0
+    out_zero_col = multiview.triangulate_batch_of_points(P2, pts, None)
+    save("dlt_degenerate.npz", proj=P.numpy(), points=pts.numpy(), conf=conf.numpy(), proj_zero_col=P2.numpy(),
+         out_zero_conf=out_zero_conf.numpy(), out_zero_col=out_zero_col.numpy())
+
+
 def main():
     op, multiview = import_reference()
     if len(sys.argv) > 1 and sys.argv[1] == "v2v_front":
@@ -332,6 +352,8 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "coord_volumes":
         golden_coord_volumes()
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "dlt_degenerate":
+        return golden_dlt_degenerate(import_reference()[1])
     if len(sys.argv) > 1 and sys.argv[1] == "chains":
         golden_chains()
         return

@@ -158,7 +158,8 @@ def test_deterministic_backward_argument_checks(lib):
     and enums as mvn_unproject_backward."""
     B, N, C, H, W = 2, 4, 8, 24, 24
     need = lib.mvn_unproject_backward_workspace_bytes(B, N, C, H, W)
-    assert need == 256 + 3 * 1024 * 4 + (B * N * C * H * W + B * N * C) * 8
+    # header, per-(frame, channel) scales (padded to 256 B), a 64-bit sum and a flag word per element
+    assert need == 256 + (B * C * 8 + 255) // 256 * 256 + (B * N * C * H * W + B * N * C) * (8 + 4)
     assert lib.mvn_unproject_backward_workspace_bytes(0, N, C, H, W) == 0
 
     def call(ws=1, ws_bytes=need, agg=0, B_=B, N_=N):

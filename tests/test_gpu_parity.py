@@ -270,6 +270,44 @@ def test_dlt_many_views_and_degenerate_confidences(device):
     assert np.abs(out.cpu().numpy() - ab0.points_3d.numpy()).max() < 0.5     # mm; f32 pixel rounding
 
 
+def test_dlt_degenerate_inputs_follow_the_reference(golden, device):
+    """SURVEY §5 'failure' row: degenerate DLT inputs give the reference's zeros / inf / nan
+    (multiview.py:147-157) without disturbing the other joints of the batch.  Fixture: the
+    reference itself on this build container's torch (tests/golden/make_golden.py
+    dlt_degenerate).
+      * a joint whose confidences are all zero: A = 0, the reference's SVD returns V = I,
+        X = -e4 and the point is (0, 0, 0) — so must ours (bit for bit, +0);
+      * cameras that do not see z (third column of every P zero): column 2 of A is exactly 0
+        and e3 is an exact null vector, so X[3] = 0 and X[:3] / X[3] = (nan, nan, +-inf).  Ours
+        detects the zero column and returns exactly that.  The reference's LAPACK returns the
+        exact e3 for 4 of the 6 joints (their NaN / inf positions must match ours; the sign of
+        the infinity is the arbitrary sign of the singular vector) and a rounding-perturbed
+        vector for the other 2 (X[3] ~ 1e-7: coordinates of ~1e7 — the degenerate limit, which
+        no other LAPACK need reproduce; on the GPU box's host the pattern differs again)."""
+    from mvn_rocm import multiview
+    d = golden("dlt_degenerate.npz")
+    P, pts, conf = (torch.from_numpy(d[k]) for k in ("proj", "points", "conf"))
+    ref = d["out_zero_conf"]
+    out = multiview.triangulate_batch_of_points(P.to(device), pts.to(device), conf.to(device)).cpu().numpy()
+    assert np.isfinite(out).all()
+    assert_bits_equal(out[0, 1], ref[0, 1])
+    assert_bits_equal(out[1, 2], ref[1, 2])
+    keep = np.ones((2, 3), bool)
+    keep[0, 1] = keep[1, 2] = False
+    x64 = restate_np.triangulate_batch_of_points(P.numpy(), pts.numpy(), conf.numpy())
+    assert max_rel(out[keep], x64[keep]) <= 1e-6          # the other joints are unaffected
+    assert max_rel(out[keep], ref[keep]) <= 1e-3          # (the f32 reference's own SVD error)
+    ref = d["out_zero_col"]
+    out = multiview.triangulate_batch_of_points(torch.from_numpy(d["proj_zero_col"]).to(device),
+                                                pts.to(device)).cpu().numpy()
+    assert np.isnan(out[..., :2]).all() and np.isinf(out[..., 2]).all()
+    exact = ~np.isfinite(ref).all(-1)                      # joints where LAPACK found e3 exactly
+    assert exact.sum() == 4
+    np.testing.assert_array_equal(np.isnan(out[exact]), np.isnan(ref[exact]))
+    np.testing.assert_array_equal(np.isinf(out[exact]), np.isinf(ref[exact]))
+    assert (np.abs(ref[~exact][:, 2]) > 1e6).all()         # the others: the degenerate limit
+
+
 def test_dlt_single_point_api(device):
     from mvn_rocm import multiview, synth
     ab = synth.algebraic_batch(1, 4, 3, seed=7)

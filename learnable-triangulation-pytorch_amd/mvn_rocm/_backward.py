@@ -16,9 +16,10 @@ from . import _lib
 from ._ops import _DTYPE_CODE, _op, _ptr, _require_gpu, _stream, call
 
 
-# Accumulation of the unprojection backward: "fixed" (default) — per-call-scaled 64-bit
-# fixed point (mvn_unproject_backward_deterministic): bit-identical across runs, the f32
-# rounding of the exact sums, and ~4x faster than "float_atomic" (mvn_unproject_backward,
+# Accumulation of the unprojection backward: "fixed" (default) — 64-bit fixed point scaled
+# per (frame, channel) plane (mvn_unproject_backward_deterministic): bit-identical across
+# runs, the f32 rounding of the exact sums above 2^-38 of the plane's bound, the reference's
+# per-element NaN / inf semantics, and ~3x faster than "float_atomic" (mvn_unproject_backward,
 # order-dependent f32 atomics; kept for A/B and for callers that want no workspace).
 UNPROJECT_BACKWARD = "fixed"
 

@@ -165,6 +165,69 @@ def timed_loop(step, args, clock):
     return clock.max_over_ranks(time.perf_counter() - t0)
 
 
+# ----------------------------------------------------------------------------- GPU telemetry
+def _smi(fn, *a):
+    try:
+        return fn(*a)
+    except Exception:       # telemetry must never fail the bench
+        return None
+
+
+def gpu_identity(device):
+    """Which MI355X the line was measured on (so that lines from different boxes can be
+    compared): ASIC serial / UUID and the board's power cap, from amdsmi."""
+    import torch
+    try:
+        import amdsmi
+        h = torch.cuda._get_amdsmi_handler(device)
+    except Exception:
+        return None
+    asic = _smi(amdsmi.amdsmi_get_gpu_asic_info, h) or {}
+    cap = _smi(amdsmi.amdsmi_get_power_cap_info, h) or {}
+    return {"uuid": _smi(amdsmi.amdsmi_get_gpu_device_uuid, h), "asic_serial": asic.get("asic_serial"),
+            "market_name": asic.get("market_name"), "power_cap_w": (cap.get("power_cap") or 0) / 1e6 or None}
+
+
+def telemetry(device, step, seconds=0.06, samples=6):
+    """Clocks, power and temperature the GPU holds under this config's load: an untimed burst
+    of the same step (~`seconds` of GPU work, right after the timed region, so the same
+    thermal and power state) is enqueued and amdsmi is sampled while it runs.  Medians of
+    `samples` reads: sclk / mclk (MHz), socket power (W), hotspot temperature (C), GFX
+    activity (%), and the throttle status word (0 = no throttling)."""
+    import statistics
+    import torch
+    try:
+        import amdsmi
+        h = torch.cuda._get_amdsmi_handler(device)
+    except Exception:
+        return None
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step(False)
+    torch.cuda.synchronize()
+    per = max(time.perf_counter() - t0, 1e-5)
+    for _ in range(max(4, int(seconds / per))):
+        step(False)
+    reads = {"sclk_mhz": [], "mclk_mhz": [], "power_w": [], "temp_hotspot_c": [], "gfx_activity_pct": [],
+             "throttle_status": []}
+    for _ in range(samples):
+        time.sleep(seconds / (2 * samples))
+        g = _smi(amdsmi.amdsmi_get_clock_info, h, amdsmi.AmdSmiClkType.GFX) or {}
+        m = _smi(amdsmi.amdsmi_get_clock_info, h, amdsmi.AmdSmiClkType.MEM) or {}
+        pw = _smi(amdsmi.amdsmi_get_power_info, h) or {}
+        mt = _smi(amdsmi.amdsmi_get_gpu_metrics_info, h) or {}
+        for k, v in (("sclk_mhz", g.get("clk", g.get("cur_clk"))), ("mclk_mhz", m.get("clk", m.get("cur_clk"))),
+                     ("power_w", pw.get("average_socket_power", pw.get("current_socket_power"))),
+                     ("temp_hotspot_c", mt.get("temperature_hotspot")), ("gfx_activity_pct", mt.get("average_gfx_activity")),
+                     ("throttle_status", mt.get("throttle_status"))):
+            if isinstance(v, (int, float)):
+                reads[k].append(v)
+    torch.cuda.synchronize()
+    out = {k: (statistics.median(v) if v else None) for k, v in reads.items()}
+    out["samples"] = samples
+    return out
+
+
 # ----------------------------------------------------------------------------- algorithmic bytes
 def unproject_bytes(c, E, cuboid=False):
     """Algorithmic bytes of one frame's unprojection: features read once,
@@ -324,11 +387,12 @@ def run_config(name, args, rank, world, device, clock, cuboid=False, cfg=None, f
     E = 2 if cfg["dtype"] == torch.bfloat16 else 4
     frames_total = wl.global_batch * args.steps
     unproj_ms, sa_ms = wl.kernel_ms()
+    tel = telemetry(device, lambda t: wl.step(t)) if world == 1 else None
     launch_bytes = unproject_bytes(cfg, E, cuboid) * cfg["frames"]
     return dict(cfg=cfg, workload=wl, elapsed=elapsed, fps=frames_total / elapsed, ms_per_step=elapsed / args.steps * 1e3,
                 unproject_ms=unproj_ms, softargmax_ms=sa_ms, launch_bytes=launch_bytes,
                 achieved_gbps=launch_bytes / (unproj_ms * 1e-3) / 1e9,
-                path_gbps=frame_bytes(cfg, E, cuboid) * frames_total / elapsed / 1e9)
+                path_gbps=frame_bytes(cfg, E, cuboid) * frames_total / elapsed / 1e9, telemetry=tel)
 
 
 def run_config5(args, rank, world, device, clock, cuboid=False):
@@ -369,6 +433,7 @@ def run_config5(args, rank, world, device, clock, cuboid=False):
 
     elapsed = timed_loop(step, args, clock)
     conv_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    tel = telemetry(device, step) if world == 1 else None
     tflops = V2V_FLOP_PER_FRAME * B / (conv_ms * 1e-3) / 1e12
     # the same work through the one-call pipeline (mvn_unproject_v2v_front: frame groups of 8
     # through a 134 MB workspace instead of the 1.07 GB whole-batch intermediate)
@@ -379,7 +444,7 @@ def run_config5(args, rank, world, device, clock, cuboid=False):
     return dict(parity_inputs=pin, workload=cfg["label"], value=B * world * args.steps / elapsed, unit="frames/s",
                 one_call={"value": B * world * args.steps / one, "ms_per_step": one / args.steps * 1e3,
                           "api": "mvn_unproject_v2v_front (groups of 8 frames, MALL-resident intermediate)"},
-                ms_per_step=elapsed / args.steps * 1e3, frames_per_gpu=B, dtype="bf16",
+                ms_per_step=elapsed / args.steps * 1e3, frames_per_gpu=B, dtype="bf16", telemetry=tel,
                 roofline={"kernel": "v2v_front<bf16> (Conv3d 32->16 k7 + BN + ReLU)", "bound": "mfma",
                           "achieved": tflops, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": tflops / MFMA_BF16_PEAK_TFLOPS, "launch_ms": conv_ms,
@@ -711,7 +776,8 @@ def main():
         secondary = dict(workload=s["cfg"]["label"], value=s["fps"], unit="frames/s", ms_per_step=s["ms_per_step"],
                          frames_per_gpu=s["cfg"]["frames"], dtype="bf16", unproject_ms=s["unproject_ms"],
                          softargmax_ms=s["softargmax_ms"], roofline=roofline(s["cfg"], s, "3", device),
-                         path_algorithmic_gbps=s["path_gbps"], path_frac=s["path_gbps"] / HBM_PEAK_GBPS)
+                         path_algorithmic_gbps=s["path_gbps"], path_frac=s["path_gbps"] / HBM_PEAK_GBPS,
+                         telemetry=s["telemetry"])
     if not args.no_secondary and not args.no_in_kernel_coords:
         # the same workload with the coordinate volume formed inside both kernels from the
         # per-frame cuboids instead of read from HBM
@@ -734,7 +800,7 @@ def main():
                     unit="frames/s", scaling="strong", global_batch=128, frames_per_gpu=count,
                     ms_per_step=r4["ms_per_step"], unproject_ms=r4["unproject_ms"],
                     unproject_achieved_gbps=r4["achieved_gbps"], unproject_frac=r4["achieved_gbps"] / HBM_PEAK_GBPS,
-                    collective="all_gather joints (RCCL)" if world > 1 else None)
+                    collective="all_gather joints (RCCL)" if world > 1 else None, telemetry=r4["telemetry"])
         cfg5 = run_config5(args, rank, world, device, clock)
         if not args.no_in_kernel_coords:
             k5 = run_config5(args, rank, world, device, clock, cuboid=True)
@@ -785,6 +851,8 @@ def main():
             "softargmax_ms": r["softargmax_ms"],
             "path_algorithmic_gbps": r["path_gbps"],
             "path_frac": r["path_gbps"] / HBM_PEAK_GBPS,
+            "telemetry": r["telemetry"],
+            "gpu": gpu_identity(device),
             "cpu_baseline": base,
             "parity": parity,
             "gather": gather,

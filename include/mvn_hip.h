@@ -163,10 +163,14 @@ int mvn_v2v_front(const void* vol_cl, const void* weight_packed, const float* sc
  * default, one group's intermediate within half of the 256 MiB MALL: 8 frames at V = 64)
  * through `workspace` (>= mvn_unproject_v2v_front_workspace_bytes(group_frames, V) bytes).
  * Replaces triangulation.py:349-352 up to V2VModel.front_layers[0] (v2v.py:145-146).
- *   C == 32, V % 16 == 0, agg != MVN_AGG_CONF, 1 <= N <= 8 views (the channels-last
- *   kernels), B >= 1 (MVN_ERR_SHAPE otherwise; mvn_rocm.v2v.unproject_v2v_front routes more
- *   views and empty batches through the two calls); exactly one of coords / cuboids non-NULL.
+ *   C == 32, V % 16 == 0, 1 <= N <= 8 views (the channels-last kernels), B >= 1
+ *   (MVN_ERR_SHAPE otherwise; mvn_rocm.v2v.unproject_v2v_front routes more views and empty
+ *   batches through the two calls); exactly one of coords / cuboids non-NULL.
  *   out (B, 16, V, V, V) out_dtype.  Bit-identical to the two calls on the whole batch.
+ * mvn_unproject_v2v_front takes agg != MVN_AGG_CONF; mvn_unproject_v2v_front_ex also takes
+ * MVN_AGG_CONF with conf (B, N, C) f32 — the volumetric model's vol_confidences whenever
+ * volume_aggregation_method starts with 'conf' (triangulation.py:268-269, 349; op.py:147-148)
+ * — and ignores conf otherwise.
  */
 size_t mvn_unproject_v2v_front_workspace_bytes(int group_frames, int V);
 int mvn_unproject_v2v_front(const void* feat, int feat_dtype, const float* proj, const float* coords,
@@ -174,6 +178,12 @@ int mvn_unproject_v2v_front(const void* feat, int feat_dtype, const float* proj,
                             const void* weight_packed, const float* scale, const float* shift, void* out,
                             int out_dtype, void* workspace, size_t workspace_bytes, int group_frames,
                             int B, int N, int C, int H, int W, int V, void* stream);
+int mvn_unproject_v2v_front_ex(const void* feat, int feat_dtype, const float* proj, const float* coords,
+                               const float* cuboids, int transfer_cmu, int agg, const float* conf,
+                               int align_corners, const void* weight_packed, const float* scale,
+                               const float* shift, void* out, int out_dtype, void* workspace,
+                               size_t workspace_bytes, int group_frames, int B, int N, int C, int H, int W,
+                               int V, void* stream);
 
 /*
  * 2D soft-argmax of heatmaps.  Replaces mvn/utils/op.py:11-47 (integrate_tensor_2d) with
@@ -257,10 +267,12 @@ int mvn_unproject_backward(const void* feat, int feat_dtype, const float* proj, 
  * contribution is scaled by a power of two 2^e and accumulated as a 64-bit integer (integer
  * adds are associative), then converted to f32 — two runs are bit-identical.  e is chosen per
  * (frame, channel) plane on the device from that plane's finite maxima of |grad_out| (and
- * |feat| for softmax, |conf| and |feat| for conf*) so that no sum of the plane can overflow;
- * an element whose exact sum is above 2^-38 of the plane's bound nvox * max|g| * factor comes
- * out as the f32 rounding of that exact sum (below, its absolute error is at most 2^-62 of
- * the bound).  Non-finite contributions follow the reference's autograd element by element: a
+ * |feat| for softmax, |conf| and |feat| for conf*) so that no sum of the plane can overflow.
+ * Each contribution is rounded to a whole unit u = 2^-62 of the plane's bound
+ * nvox * max|g| * factor before it is added, so an element fed by n contributions comes out
+ * as the f32 rounding of an integer sum within n/2 units of its exact sum: absolute error
+ * <= n/2 * u + half an f32 ulp (relative <= n * 2^-25 + 2^-24 once the element is above
+ * 2^-38 of the bound, i.e. 2^24 units).  Non-finite contributions follow the reference's autograd element by element: a
  * NaN / inf grad_out, feature or confidence reaches exactly the gradient elements it reaches
  * in ATen's grid_sampler / softmax / mul backward (NaN if a NaN or both infinities meet there,
  * else the infinity); every other element stays finite.

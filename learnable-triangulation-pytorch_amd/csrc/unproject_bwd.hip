@@ -26,11 +26,12 @@
 // the order the waves and blocks arrive in and two runs are bit-identical.  e is chosen per
 // (frame, channel) plane — every element of grad_feat[b, :, c] and grad_conf[b, :, c] shares
 // it — on the device (fix_scale_planes: no host sync) from that plane's finite maxima, so
-// that no sum of the plane can leave +-2^62.  Range: the unit is 2^-62 of the plane's bound
-// nvox * max|g| * factor, so an element keeps all 24 bits when its exact sum is above
-// 2^-38 of that bound (2^-20 of max|g| * factor at 64^3) and is then the f32 rounding of the
-// exact sum; below, its absolute error is at most the unit (a frame or channel whose gradients
-// are 1e8 x smaller than another's has its own scale).
+// that no sum of the plane can leave +-2^62.  Range: the unit u is 2^-62 of the plane's bound
+// nvox * max|g| * factor; each contribution is rounded to a whole unit, so an element fed by n
+// contributions is the f32 rounding of an integer sum within n/2 units of its exact sum —
+// absolute error <= n/2 * u + half an f32 ulp, i.e. relative <= n * 2^-25 + 2^-24 once the
+// element is above 2^24 units = 2^-38 of the bound (2^-20 of max|g| * factor at 64^3); a frame
+// or channel whose gradients are 1e8 x smaller than another's has its own scale.
 // Non-finite contributions (a NaN or infinite grad_out / feature / confidence reaching a tap)
 // are not summed: they set per-element flags (NaN, +inf, -inf) with atomicOr, and the element
 // comes out as the reference's sequential float sum would: NaN if a NaN or both infinities
@@ -189,7 +190,10 @@ __global__ __launch_bounds__(kThreads) void unproject_bwd_tiled(
 
   const TG* gb = gout + size_t(b) * C * nvox + vox;
   if (total < 0) {
-    // footprint larger than the LDS budget: scatter every tap with a global atomic
+    // footprint larger than the LDS budget: scatter every tap with a global atomic.  Threads
+    // past the volume's edge (partial tiles) have no voxel: they scatter nothing (their taps
+    // sit at voxel 0's coordinates, where 0 * an infinite coefficient would add a NaN)
+    if (!act) return;
     for (int c = 0; c < C; ++c) {
       float s[NV];
 #pragma unroll

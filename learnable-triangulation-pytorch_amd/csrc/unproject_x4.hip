@@ -43,15 +43,10 @@ template <int K> struct X4Shape;
 template <> struct X4Shape<0> {   // 4 views, f32 maps
   static constexpr int NV = 4, G = 4, TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, MC = 2, WAVES = 4;
   static constexpr int STORE_F32 = kStorePolicyF32;
-  static constexpr bool B16 = false;
 };
-#ifndef MVN_X4_B16SLOT
-#define MVN_X4_B16SLOT 0
-#endif
-template <> struct X4Shape<2> {   // 4 views, bf16 maps
-  static constexpr int NV = 4, G = 4, TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = MVN_X4_B16SLOT ? 2048 : 1024, MC = 2, WAVES = 4;
+template <> struct X4Shape<2> {   // 4 views, bf16 maps (widened exactly to f32 slots when staged)
+  static constexpr int NV = 4, G = 4, TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 1024, MC = 2, WAVES = 4;
   static constexpr int STORE_F32 = kStorePolicyF32;
-  static constexpr bool B16 = MVN_X4_B16SLOT;   // slots of 4 bf16 channels (8 bytes), widened per tap
 };
 // 8 views (BASELINE config 4, CMU-style): the footprint of 8 views doubles, so slots of 2
 // channels (8 bytes) keep two 2,048-slot buffers in 32 KiB (footprints of a 4x8x8 tile at
@@ -62,22 +57,15 @@ template <> struct X4Shape<2> {   // 4 views, bf16 maps
 template <> struct X4Shape<3> {
   static constexpr int NV = 8, G = 2, TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 2048, MC = 3, WAVES = 3;
   static constexpr int STORE_F32 = 0;
-  static constexpr bool B16 = false;
 };
 
 // LDS slot: one pixel's G channels as f32
-template <int G, bool B16> struct SlotT;
-template <> struct SlotT<4, false> { using type = uint4; };
-template <> struct SlotT<2, false> { using type = uint2; };
-template <> struct SlotT<4, true> { using type = uint2; };   // 4 bf16 channels
+template <int G> struct SlotT;
+template <> struct SlotT<4> { using type = uint4; };
+template <> struct SlotT<2> { using type = uint2; };
 // channel pair q of a slot
 __device__ __forceinline__ f2 slot_pair(const uint4& s, int q) { return q ? hi2(s) : lo2(s); }
 __device__ __forceinline__ f2 slot_pair(const uint2& s, int) { return f2{__uint_as_float(s.x), __uint_as_float(s.y)}; }
-// channel pair q of a 4-bf16-channel slot, widened exactly (lo half: shift, hi half: mask)
-__device__ __forceinline__ f2 slot_pair_b16(const uint2& s, int q) {
-  const uint32_t d = q ? s.y : s.x;
-  return f2{__uint_as_float(d << 16), __uint_as_float(d & 0xffff0000u)};
-}
 
 // Per-view LDS regions (block-uniform, scalar registers), packed 3 words per view —
 // (x0 + 1, y0 + 1), (bw, bh), sbase | cbase << 13 | pass << 24 — the derived fields
@@ -137,12 +125,12 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   constexpr int kZeroSlot = kBuf - 2, kTrash = kBuf - 2 - kWave;
   // LDS slot = one pixel's G channels as f32 (16 / 8 bytes; bf16 maps are widened exactly
   // when staged: bf16 slots halve the LDS bytes but the per-tap widening costs more VALU, r13)
-  constexpr bool B16 = S::B16;
-  using Slot = typename SlotT<G, B16>::type;
+  using Slot = typename SlotT<G>::type;
   constexpr uint32_t kSlotB = sizeof(Slot);
   constexpr uint32_t E = sizeof(TIn);
 
-  __shared__ Slot stage[2 * kBuf];
+  __shared__ Slot stageA[kBuf];
+  __shared__ Slot stageB[kBuf];
   __shared__ int red[kWaves][NV][4];
 
   // ---- which tile (z-tiles fastest; block order as unproject_tiled) ------------------
@@ -167,7 +155,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   const TIn* fb = feat + size_t(b) * NV * C * HW;
   const float* cfb = conf ? conf + size_t(b) * NV * C : nullptr;
 
-  if (t < 4) stage[(t >> 1) * kBuf + kZeroSlot + (t & 1)] = Slot{};
+  if (t < 4) (t < 2 ? stageA : stageB)[kZeroSlot + (t & 1)] = Slot{};
 
   const int X0 = tx * TX, Y0 = ty * TY, Z0 = tz * TZ;
 
@@ -378,13 +366,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       Slot q;
-      if constexpr (B16) {
-        // pixel p's bf16 of channels (0, 1) and (2, 3), one v_perm_b32 each
-        const uint32_t sel = (p & 1) ? 0x07060302u : 0x05040100u;
-        const uint32_t w0 = p < 2 ? pre[0].x : pre[0].y, w1 = p < 2 ? pre[1].x : pre[1].y;
-        const uint32_t w2 = p < 2 ? pre[2].x : pre[2].y, w3 = p < 2 ? pre[3].x : pre[3].y;
-        q = make_uint2(__builtin_amdgcn_perm(w1, w0, sel), __builtin_amdgcn_perm(w3, w2, sel));
-      } else if constexpr (G == 4)
+      if constexpr (G == 4)
         q = make_uint4(chunk_px(pre[0], p), chunk_px(pre[1], p), chunk_px(pre[2], p), chunk_px(pre[3], p));
       else
         q = make_uint2(chunk_px(pre[0], p), chunk_px(pre[1], p));
@@ -422,14 +404,9 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       const Slot d = tap(buf + asw[v] + kSlotB);
       const f2 w0 = splat<0>(wp[v][0]), w1 = splat<1>(wp[v][0]), w2 = splat<0>(wp[v][1]), w3 = splat<1>(wp[v][1]);
 #pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        if constexpr (B16)
-          sv[q][v] = pk_fma(slot_pair_b16(d, q), w3,
-                            pk_fma(slot_pair_b16(cq, q), w2, pk_fma(slot_pair_b16(bq, q), w1, slot_pair_b16(a, q) * w0)));
-        else
-          sv[q][v] = pk_fma(slot_pair(d, q), w3,
-                            pk_fma(slot_pair(cq, q), w2, pk_fma(slot_pair(bq, q), w1, slot_pair(a, q) * w0)));
-      }
+      for (int q = 0; q < NP; ++q)
+        sv[q][v] = pk_fma(slot_pair(d, q), w3,
+                          pk_fma(slot_pair(cq, q), w2, pk_fma(slot_pair(bq, q), w1, slot_pair(a, q) * w0)));
       if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight
     }
   };
@@ -534,32 +511,28 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     };
     issue(0);
     tap_slots();
-    commit(stage);
+    commit(stageA);
     __syncthreads();
     // A group's outputs are stored after the NEXT group's commit: on gfx950 vmcnt counts
     // stores as well as loads, in issue order, so stores issued at the end of a consume made
     // the commit's wait for the next group's loads also wait for their write acknowledgement.
     float r[G];
-#ifndef MVN_X4_DIAG
-#define MVN_X4_DIAG 0
-#endif
-    const int Cl = MVN_X4_DIAG == 1 ? G : C;     // diagnostic: prologue + first group only
-    for (int c0 = 0; c0 < Cl; c0 += 2 * G) {
-      const bool more1 = c0 + G < Cl, more2 = c0 + 2 * G < Cl;
+    for (int c0 = 0; c0 < C; c0 += 2 * G) {
+      const bool more1 = c0 + G < C, more2 = c0 + 2 * G < C;
       if (more1) issue(c0 + G);
-      consume(stage, c0, r);
+      consume(stageA, c0, r);
       if (!more1) { store_out(c0, r); break; }
-      commit(stage + kBuf);
+      commit(stageB);
       __builtin_amdgcn_sched_barrier(0);
       store_out(c0, r);
-      if (MVN_X4_DIAG != 2) __syncthreads();
+      __syncthreads();
       if (more2) issue(c0 + 2 * G);
-      consume(stage + kBuf, c0 + G, r);
+      consume(stageB, c0 + G, r);
       if (!more2) { store_out(c0 + G, r); break; }
-      commit(stage);
+      commit(stageA);
       __builtin_amdgcn_sched_barrier(0);
       store_out(c0 + G, r);
-      if (MVN_X4_DIAG != 2) __syncthreads();
+      __syncthreads();
     }
     return;
   }
@@ -580,11 +553,11 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
           chunk_fields(rv, v, li, goff, s0, mask, true);
           Chunk pre[G];
           load_group(pre, goff, c0);
-          write_group(stage, pre, s0, mask);
+          write_group(stageA, pre, s0, mask);
         }
       }
       __syncthreads();
-      sample_views(reinterpret_cast<const char*>(stage), false, pass, sv);
+      sample_views(reinterpret_cast<const char*>(stageA), false, pass, sv);
       __syncthreads();
     }
     float r[G];

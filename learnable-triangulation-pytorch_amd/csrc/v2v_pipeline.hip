@@ -29,14 +29,15 @@ extern "C" size_t mvn_unproject_v2v_front_workspace_bytes(int group_frames, int 
   return size_t(G) * size_t(V) * V * V * kCin * 2;
 }
 
-extern "C" int mvn_unproject_v2v_front(const void* feat, int feat_dtype, const float* proj, const float* coords,
-                                       const float* cuboids, int transfer_cmu, int agg, int align_corners,
-                                       const void* weight_packed, const float* scale, const float* shift, void* out,
-                                       int out_dtype, void* workspace, size_t workspace_bytes, int group_frames,
-                                       int B, int N, int C, int H, int W, int V, void* stream) {
+extern "C" int mvn_unproject_v2v_front_ex(const void* feat, int feat_dtype, const float* proj, const float* coords,
+                                          const float* cuboids, int transfer_cmu, int agg, const float* conf,
+                                          int align_corners, const void* weight_packed, const float* scale,
+                                          const float* shift, void* out, int out_dtype, void* workspace,
+                                          size_t workspace_bytes, int group_frames, int B, int N, int C, int H, int W,
+                                          int V, void* stream) {
   if (!feat || !proj || !weight_packed || !scale || !shift || !out) return MVN_ERR_ARG;
   if ((coords == nullptr) == (cuboids == nullptr)) return MVN_ERR_ARG;       // exactly one coordinate source
-  if (agg == MVN_AGG_CONF) return MVN_ERR_ARG;                               // no per-view confidences here
+  if (agg == MVN_AGG_CONF && !conf) return MVN_ERR_ARG;                      // conf*: per-view confidences
   if (B <= 0 || N <= 0 || H <= 0 || W <= 0 || V <= 0) return MVN_ERR_SHAPE;
   if (C != kCin || V % 16 != 0 || V > 256) return MVN_ERR_SHAPE;
   if (feat_dtype != MVN_DTYPE_F32 && feat_dtype != MVN_DTYPE_BF16) return MVN_ERR_DTYPE;
@@ -50,10 +51,11 @@ extern "C" int mvn_unproject_v2v_front(const void* feat, int feat_dtype, const f
     const int n = B - g < G ? B - g : G;
     const char* f = static_cast<const char*>(feat) + size_t(g) * feat_frame;
     const float* P = proj + size_t(g) * N * 12;
+    const float* cf = agg == MVN_AGG_CONF ? conf + size_t(g) * N * C : nullptr;    // (B, N, C) rows of the group
     int rc = cuboids ? mvn_unproject_cuboid(f, feat_dtype, P, cuboids + size_t(g) * MVN_CUBOID_FLOATS, transfer_cmu,
-                                            nullptr, workspace, MVN_DTYPE_BF16, MVN_LAYOUT_NDHWC, n, N, C, H, W, V,
+                                            cf, workspace, MVN_DTYPE_BF16, MVN_LAYOUT_NDHWC, n, N, C, H, W, V,
                                             agg, align_corners, stream)
-                     : mvn_unproject_ex(f, feat_dtype, P, coords + size_t(g) * vox * 3, nullptr, workspace,
+                     : mvn_unproject_ex(f, feat_dtype, P, coords + size_t(g) * vox * 3, cf, workspace,
                                         MVN_DTYPE_BF16, MVN_LAYOUT_NDHWC, n, N, C, H, W, V, V, V, agg, align_corners,
                                         stream);
     if (rc != MVN_OK) return rc;
@@ -62,4 +64,15 @@ extern "C" int mvn_unproject_v2v_front(const void* feat, int feat_dtype, const f
     if (rc != MVN_OK) return rc;
   }
   return MVN_OK;
+}
+
+extern "C" int mvn_unproject_v2v_front(const void* feat, int feat_dtype, const float* proj, const float* coords,
+                                       const float* cuboids, int transfer_cmu, int agg, int align_corners,
+                                       const void* weight_packed, const float* scale, const float* shift, void* out,
+                                       int out_dtype, void* workspace, size_t workspace_bytes, int group_frames,
+                                       int B, int N, int C, int H, int W, int V, void* stream) {
+  if (agg == MVN_AGG_CONF) return MVN_ERR_ARG;        // conf*: mvn_unproject_v2v_front_ex with the confidences
+  return mvn_unproject_v2v_front_ex(feat, feat_dtype, proj, coords, cuboids, transfer_cmu, agg, nullptr,
+                                    align_corners, weight_packed, scale, shift, out, out_dtype, workspace,
+                                    workspace_bytes, group_frames, B, N, C, H, W, V, stream);
 }

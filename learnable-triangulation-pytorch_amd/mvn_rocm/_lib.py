@@ -50,6 +50,9 @@ SIGNATURES = {
     "mvn_unproject_v2v_front": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_size_t,
                                          _c_int] + [_c_int] * 6 + [_c_void_p]),
+    "mvn_unproject_v2v_front_ex": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int,
+                                            _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int,
+                                            _c_void_p, _c_size_t, _c_int] + [_c_int] * 6 + [_c_void_p]),
     "mvn_v2v_front_packed_weight_bytes": (_c_size_t, []),
     "mvn_v2v_front": (_c_int, [_c_void_p] * 5 + [_c_int, _c_int, _c_int, _c_void_p]),
     "mvn_unproject_backward": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int,

@@ -62,20 +62,23 @@ def v2v_front(vol_cl, packed, scale, shift, out_dtype=torch.float32):
 
 
 def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggregation_method="softmax",
-                            out_dtype=torch.bfloat16, align_corners=False):
+                            out_dtype=torch.bfloat16, align_corners=False, vol_confidences=None):
     """unproject_heatmaps (op.py:99-163) written channels-last: (B, Vx, Vy, Vz, C).
-    ``coord_volumes`` may be a ``volumetric.Cuboids`` (coordinates formed in-kernel)."""
+    ``coord_volumes`` may be a ``volumetric.Cuboids`` (coordinates formed in-kernel);
+    ``vol_confidences`` (B, N, C) is read for 'conf*' aggregation (op.py:147-148), as
+    ``unproject_heatmaps``'s."""
     from .volumetric import Cuboids
     agg = aggregation_code(volume_aggregation_method)
-    if agg == _lib.MVN_AGG_CONF:
-        raise ValueError("unproject_channels_last: 'conf*' aggregation is not supported here")
     cub = coord_volumes if isinstance(coord_volumes, Cuboids) else None
-    feat, proj, _ = unproject_inputs(heatmaps, proj_matricies, None, agg, volume_aggregation_method, cub)
+    feat, proj, conf = unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, volume_aggregation_method, cub)
+    if conf is not None:
+        _require_gpu(feat, conf)
+    cptr = conf.data_ptr() if conf is not None else None
     if feat.dtype == torch.float32 and out_dtype == torch.bfloat16:
         # f32 maps into a bf16 volume: the kernels write f32 (no f32 -> bf16 instantiation,
         # mvn_hip.h), rounded to nearest-even by one device cast
         return unproject_channels_last(feat, proj, coord_volumes, volume_aggregation_method, torch.float32,
-                                       align_corners).to(torch.bfloat16)
+                                       align_corners, conf).to(torch.bfloat16)
     fd, od = _dtype_code(feat.dtype), _dtype_code(out_dtype)
     B, N, C, H, W = feat.shape
     if N > 8:
@@ -84,8 +87,8 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
         from .op import unproject_heatmaps
         # written in out_dtype by the kernel itself (bf16 maps into an f32 volume keep f32
         # precision)
-        vol = unproject_heatmaps(feat, proj, coord_volumes, volume_aggregation_method, align_corners=align_corners,
-                                 out_dtype=out_dtype)
+        vol = unproject_heatmaps(feat, proj, coord_volumes, volume_aggregation_method, conf,
+                                 align_corners=align_corners, out_dtype=out_dtype)
         return vol.permute(0, 2, 3, 4, 1).contiguous()
     if cub is not None:
         # coordinates formed in-kernel from the per-frame cuboids (bit-identical)
@@ -96,7 +99,7 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
         if out.numel() == 0:
             return out
         code = _lib.load().mvn_unproject_cuboid(feat.data_ptr(), fd, proj.data_ptr(), cub.params.data_ptr(),
-                                                int(cub.transfer), None, out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC,
+                                                int(cub.transfer), cptr, out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC,
                                                 B, N, C, H, W, V, agg, int(align_corners), _stream(feat))
         _lib.check(code, "mvn_unproject_cuboid")
         return out
@@ -108,7 +111,7 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
     out = torch.empty((B, Vx, Vy, Vz, C), dtype=out_dtype, device=feat.device)
     if out.numel() == 0:                  # empty batch: the empty volume, as unproject_heatmaps
         return out
-    code = _lib.load().mvn_unproject_ex(feat.data_ptr(), fd, proj.data_ptr(), coords.data_ptr(), None,
+    code = _lib.load().mvn_unproject_ex(feat.data_ptr(), fd, proj.data_ptr(), coords.data_ptr(), cptr,
                                         out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC, B, N, C, H, W, Vx, Vy, Vz, agg,
                                         int(align_corners), _stream(feat))
     _lib.check(code, "mvn_unproject_ex")
@@ -136,18 +139,17 @@ class Basic3DBlockFront(nn.Module):
 
 def unproject_v2v_front(heatmaps, proj_matricies, coord_volumes, packed, scale, shift,
                         volume_aggregation_method="softmax", out_dtype=torch.float32, group_frames=0,
-                        align_corners=False):
+                        align_corners=False, vol_confidences=None):
     """Config 5 in one call (``mvn_unproject_v2v_front``): unproject_heatmaps (op.py:99-163)
     written channels-last bf16, then the front block relu(bn(conv3d_7)), pipelined over frame
     groups through a workspace of one group's intermediate (default: 8 frames at V = 64,
     within half of the MALL).  ``coord_volumes`` may be a ``volumetric.Cuboids``.  Equal to
-    ``v2v_front(unproject_channels_last(...))`` bit for bit."""
+    ``v2v_front(unproject_channels_last(...))`` bit for bit.  'conf*' aggregation reads
+    ``vol_confidences`` (B, N, C), as the volumetric model does (triangulation.py:349)."""
     from .volumetric import Cuboids
     agg = aggregation_code(volume_aggregation_method)
-    if agg == _lib.MVN_AGG_CONF:
-        raise ValueError("unproject_v2v_front: 'conf*' aggregation is not supported here")
     cub = coord_volumes if isinstance(coord_volumes, Cuboids) else None
-    feat, proj, _ = unproject_inputs(heatmaps, proj_matricies, None, agg, volume_aggregation_method, cub)
+    feat, proj, conf = unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, volume_aggregation_method, cub)
     fd, od = _dtype_code(feat.dtype), _dtype_code(out_dtype)
     B, N, C, H, W = feat.shape
     if C != CIN:
@@ -155,7 +157,8 @@ def unproject_v2v_front(heatmaps, proj_matricies, coord_volumes, packed, scale, 
     if N > 8 or B == 0:
         # more than 8 views (the channels-last kernels take N <= 8) or an empty batch: the two
         # steps, which handle both
-        cl = unproject_channels_last(feat, proj, coord_volumes, volume_aggregation_method, align_corners=align_corners)
+        cl = unproject_channels_last(feat, proj, coord_volumes, volume_aggregation_method, align_corners=align_corners,
+                                     vol_confidences=conf)
         return v2v_front(cl, packed, scale, shift, out_dtype)
     if cub is not None:
         coords, V = None, cub.volume_size
@@ -166,15 +169,19 @@ def unproject_v2v_front(heatmaps, proj_matricies, coord_volumes, packed, scale, 
             raise RuntimeError(f"coord_volumes must be ({B}, V, V, V, 3), got {tuple(coords.shape)}")
         V = coords.shape[1]
         _require_gpu(feat, proj, coords, packed, scale, shift)
+    if conf is not None:
+        _require_gpu(feat, conf)
     lib = _lib.load()
     ws = torch.empty(lib.mvn_unproject_v2v_front_workspace_bytes(int(group_frames), V), dtype=torch.uint8,
                      device=feat.device)
     out = torch.empty((B, COUT, V, V, V), dtype=out_dtype, device=feat.device)
-    code = lib.mvn_unproject_v2v_front(feat.data_ptr(), fd, proj.data_ptr(),
-                                       coords.data_ptr() if coords is not None else None,
-                                       cub.params.data_ptr() if cub is not None else None,
-                                       int(cub.transfer) if cub is not None else 0, agg, int(align_corners),
-                                       packed.data_ptr(), scale.data_ptr(), shift.data_ptr(), out.data_ptr(), od,
-                                       ws.data_ptr(), ws.numel(), int(group_frames), B, N, C, H, W, V, _stream(feat))
-    _lib.check(code, "mvn_unproject_v2v_front")
+    code = lib.mvn_unproject_v2v_front_ex(feat.data_ptr(), fd, proj.data_ptr(),
+                                          coords.data_ptr() if coords is not None else None,
+                                          cub.params.data_ptr() if cub is not None else None,
+                                          int(cub.transfer) if cub is not None else 0, agg,
+                                          conf.data_ptr() if conf is not None else None, int(align_corners),
+                                          packed.data_ptr(), scale.data_ptr(), shift.data_ptr(), out.data_ptr(), od,
+                                          ws.data_ptr(), ws.numel(), int(group_frames), B, N, C, H, W, V,
+                                          _stream(feat))
+    _lib.check(code, "mvn_unproject_v2v_front_ex")
     return out

@@ -132,7 +132,8 @@ def test_python_api_error_types_match_reference():
 
 def test_unproject_v2v_front_argument_validation(lib):
     """The one-call config-5 pipeline: exactly one coordinate source, 32 channels, V % 16,
-    no 'conf' aggregation, a workspace of one group (no HIP call on these paths)."""
+    'conf' aggregation only through the _ex form, a workspace of one group (no HIP call on
+    these paths)."""
     assert lib.mvn_unproject_v2v_front_workspace_bytes(8, 64) == 8 * 64 ** 3 * 32 * 2
     assert lib.mvn_unproject_v2v_front_workspace_bytes(0, 64) == 8 * 64 ** 3 * 32 * 2     # default: 8 frames
     ws = lib.mvn_unproject_v2v_front_workspace_bytes(2, 64)
@@ -149,6 +150,24 @@ def test_unproject_v2v_front_argument_validation(lib):
     assert call(V=40) == -2
     assert call(ws=None) == -5
     assert call(wsb=ws - 1) == -5
+
+    # the _ex form takes 'conf*' with the (B, N, C) confidences (triangulation.py:349)
+    def call_ex(**k):
+        return lib.mvn_unproject_v2v_front_ex(1, 0, 1, 1, None, 0, k.get("agg", 3), k.get("conf", None), 0, 1, 1, 1,
+                                              1, 0, k.get("ws", 1), ws, 2, 3, 4, 32, 96, 96, 64, None)
+    assert call_ex(agg=3, conf=None) == -1               # conf* without confidences
+    assert call_ex(agg=3, conf=1, ws=None) == -5         # (validated up to the workspace: no HIP call)
+
+
+def test_channels_last_conf_needs_confidences():
+    """'conf*' on the channels-last and one-call config-5 paths needs vol_confidences, as
+    unproject_heatmaps does (TypeError before any device work)."""
+    from mvn_rocm import v2v
+    feat, P, coords = torch.zeros(1, 4, 32, 8, 8), torch.zeros(1, 4, 3, 4), torch.zeros(1, 16, 16, 16, 3)
+    with pytest.raises(TypeError, match="vol_confidences"):
+        v2v.unproject_channels_last(feat, P, coords, "conf_norm")
+    with pytest.raises(TypeError, match="vol_confidences"):
+        v2v.unproject_v2v_front(feat, P, coords, None, None, None, "conf")
 
 
 def test_deterministic_backward_argument_checks(lib):

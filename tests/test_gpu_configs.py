@@ -162,6 +162,42 @@ def test_cfg5_one_call_pipeline_equals_two_steps(device, coords_kind):
             assert torch.equal(got, ref), (od, gf)
 
 
+@pytest.mark.parametrize("coords_kind", ("volume", "cuboids"))
+def test_cfg5_conf_aggregation_channels_last_and_one_call(device, coords_kind):
+    """'conf*' aggregation (op.py:147-148; the volumetric model with a conf-prefixed
+    volume_aggregation_method, triangulation.py:268-269, 349) on the config-5 paths at V = 64:
+    the channels-last bf16 volume is the bf16 rounding of the C oracle's bit-exact f32 volume,
+    bit for bit, and the one-call pipeline (ragged groups, default groups) equals the two
+    calls bit for bit."""
+    from mvn_rocm import synth, v2v, volumetric
+    vb = synth.volumetric_batch(3, dtype=torch.bfloat16, device=device, seed=57)
+    conf = np.random.default_rng(57).uniform(0.05, 1.0, (3, 4, 32)).astype(np.float32)
+    conf_d = _t(conf, device)
+    coords, coords_np = vb.coords, vb.coords.cpu().numpy()
+    if coords_kind == "cuboids":
+        rng = np.random.default_rng(57)
+        base = rng.uniform(-500, 500, (3, 3)) + np.array([0, 0, 900.0])
+        coords = volumetric.build_cuboids(base, 2500.0, 64, rng.uniform(0, 2 * np.pi, 3), "coco", False, device=device)
+        coords_np = coords.coord_volumes().cpu().numpy()
+    cl = v2v.unproject_channels_last(vb.features, vb.proj, coords, "conf_norm", vol_confidences=conf_d)
+    feat32 = vb.features.float().cpu().numpy()
+    for f in range(3):
+        ref = capi.unproject(feat32[f:f + 1], vb.proj[f:f + 1].cpu().numpy(), coords_np[f:f + 1], "conf",
+                             conf[f:f + 1])
+        ref_cl = torch.from_numpy(ref).permute(0, 2, 3, 4, 1).contiguous().bfloat16()
+        assert np.array_equal(bf16_bits(cl[f:f + 1]), bf16_bits(ref_cl)), f
+    g = torch.Generator().manual_seed(57)
+    w = torch.randn((16, 32, 7, 7, 7), generator=g) * 0.02
+    packed, scale, shift = v2v.fold_basic3d_block(w, torch.randn(16, generator=g) * 0.1, torch.rand(16, generator=g) + 0.5,
+                                                  torch.randn(16, generator=g) * 0.1, torch.zeros(16), torch.ones(16),
+                                                  device=device)
+    ref = v2v.v2v_front(cl, packed, scale, shift, torch.float32)
+    for gf in (2, 0):
+        got = v2v.unproject_v2v_front(vb.features, vb.proj, coords, packed, scale, shift, "conf", torch.float32, gf,
+                                      vol_confidences=conf_d)
+        assert torch.equal(got, ref), gf
+
+
 def test_v2v_front_two_frames_64(device):
     """Two frames at V = 64 (the x-column walk over 16 tiles, both frames' halos)."""
     import torch.nn.functional as F
@@ -174,6 +210,25 @@ def test_v2v_front_two_frames_64(device):
     y = v2v.v2v_front(x.permute(0, 2, 3, 4, 1).contiguous().to(device).to(torch.bfloat16), packed, scale, shift)
     ref = torch.relu(F.conv3d(x, w, None, padding=3))
     assert max_rel(y.cpu().numpy(), ref.numpy()) <= 1e-4
+
+
+@pytest.mark.parametrize("cfg", ("cfg2", "cfg4"))
+def test_frames_are_independent_of_the_batch(device, cfg):
+    """What the multi-GPU bench's gather check (bench.verify_gather) relies on: a frame's
+    unprojection and soft-argmax do not depend on the batch it is launched in.  The first and
+    the last frame of a config-2 (8 frames, 4 views, f32) / config-4-shaped (4 frames, 8
+    views) batch equal, bit for bit, the same frames launched alone (batch 1)."""
+    from mvn_rocm import op, synth
+    B, NV = (8, 4) if cfg == "cfg2" else (4, 8)
+    vb = synth.volumetric_batch(B, n_views=NV, device=device, seed=58)
+    vol = op.unproject_heatmaps(vb.features, vb.proj, vb.coords, "softmax")
+    xyz, sm = op.integrate_tensor_3d_with_coordinates(vol[:, :17], vb.coords, True)
+    for f in (0, B - 1):
+        v1 = op.unproject_heatmaps(vb.features[f:f + 1], vb.proj[f:f + 1], vb.coords[f:f + 1], "softmax")
+        x1, s1 = op.integrate_tensor_3d_with_coordinates(v1[:, :17], vb.coords[f:f + 1], True)
+        assert torch.equal(v1, vol[f:f + 1]), f
+        assert torch.equal(x1, xyz[f:f + 1]), f
+        assert torch.equal(s1, sm[f:f + 1]), f
 
 
 # ----------------------------------------------------------------------------- caller chains

@@ -110,12 +110,16 @@ template <int NV> struct RegionSet {
   }
 };
 
-template <int AGG, typename TIn, typename TOut, int K>
+// CL: channels-last output (config 5) — a compile-time layout, so that the NCDHW kernels'
+// output stores are straight-line code: the compiler's vmcnt for a staging commit then counts
+// exactly the stores issued after the loads it waits for.
+template <int AGG, typename TIn, typename TOut, int K, int CL>
 __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_per_eu(X4Shape<K>::WAVES))) void unproject_x4(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ cub, int transfer, const float* __restrict__ conf, TOut* __restrict__ out, int B,
-    int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, int budget, int out_cl) {
+    int C, int H, int W, int Vx, int Vy, int Vz, int align_corners, int budget) {
   using S = X4Shape<K>;
+  constexpr bool out_cl = CL != 0;
   constexpr int NV = S::NV, G = S::G, NP = G / 2;      // NP channel pairs per group
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ;
   constexpr int kThreads = S::THREADS, kBuf = S::SLOTS, MC = S::MC, kWaves = kThreads / kWave;
@@ -431,7 +435,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   // record (config 5).  bf16 NCDHW planes are direct 2-byte stores (r14: once the stores were
   // deferred past the next commit they beat 16-byte rows gathered through LDS, 542 -> 530 us).
   auto store_out = [&](int c0, const float (&r)[G]) __attribute__((always_inline)) {
-    if constexpr (G == 4) if (out_cl) {      // (launch_x4 sends channels-last 8-view calls to the tiled kernel)
+    if constexpr (G == 4 && CL != 0) {      // (launch_x4 sends channels-last 8-view calls to the tiled kernel)
       // c0 is block-uniform; readfirstlane keeps it scalar (soffset operands must be SGPRs)
       const uint32_t soff = __builtin_amdgcn_readfirstlane(uint32_t(c0) * uint32_t(sizeof(TOut)));
       if constexpr (sizeof(TOut) == 2) {
@@ -584,28 +588,31 @@ int launch_x4(const void* feat, const float* P, const float* coords, const float
     return MVN_ERR_SHAPE;
   const int knob = unproject_lds_slot_budget();
   const int budget = knob > 0 ? knob : 1 << 30;
-  auto go = [&](auto shape) {
-    constexpr int K = decltype(shape)::value;
+  auto go = [&](auto shape, auto cl) {
+    constexpr int K = decltype(shape)::value, CL = decltype(cl)::value;
     using S = X4Shape<K>;
     const long long nb = (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) *
                          ((Vz + S::TZ - 1) / S::TZ);
     if (nb > INT_MAX) return MVN_ERR_SHAPE;
-    unproject_x4<AGG, TIn, TOut, K><<<int(nb), S::THREADS, 0, s>>>(
+    unproject_x4<AGG, TIn, TOut, K, CL><<<int(nb), S::THREADS, 0, s>>>(
         static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, C, H, W, Vx, Vy,
-        Vz, align_corners, budget, out_cl);
+        Vz, align_corners, budget);
     return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
   };
-  if (eight) return go(std::integral_constant<int, 3>{});
-  return go(std::integral_constant<int, sizeof(TIn) == 2 ? 2 : 0>{});
+  using NC = std::integral_constant<int, 0>;
+  using CLv = std::integral_constant<int, 1>;
+  if (eight) return go(std::integral_constant<int, 3>{}, NC{});
+  using K4 = std::integral_constant<int, sizeof(TIn) == 2 ? 2 : 0>;
+  return out_cl ? go(K4{}, CLv{}) : go(K4{}, NC{});
 }
 
 // Diagnostics (mvn_debug_unproject_occupancy): resident blocks per CU of the softmax kernels.
 int x4_blocks_per_cu(int bf16) {
   int n = 0;
   const hipError_t e =
-      bf16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, unproject_x4<MVN_AGG_SOFTMAX, uint16_t, uint16_t, 2>,
+      bf16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, unproject_x4<MVN_AGG_SOFTMAX, uint16_t, uint16_t, 2, 0>,
                                                           X4Shape<2>::THREADS, 0)
-           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, unproject_x4<MVN_AGG_SOFTMAX, float, float, 0>,
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, unproject_x4<MVN_AGG_SOFTMAX, float, float, 0, 0>,
                                                           X4Shape<0>::THREADS, 0);
   return e == hipSuccess ? n : MVN_ERR_LAUNCH;
 }

@@ -1,7 +1,8 @@
 """ORACLE — test infrastructure only.
 
-float64 restatements: the 2D soft-argmax (mvn/utils/op.py:11-47) and the
-confidence-weighted DLT (mvn/utils/multiview.py:132-174).
+float64 restatements: the 2D soft-argmax (mvn/utils/op.py:11-47), the
+confidence-weighted DLT (mvn/utils/multiview.py:132-174) and the 'sum' unprojection's
+feature gradient (the exact sum of the forward's f32 tap products).
 The design matrix is formed in float32 with the reference's three separately rounded
 ops (multiview.py:150-152) and only the null-space solve is promoted to float64
 (LAPACK gesdd via numpy).  This is the gate for the HIP DLT (<= 1e-6 relative): the
@@ -108,3 +109,56 @@ def nearest_voxel(coords, keypoints):
     sq = (d * d).astype(f)
     d2 = ((sq[..., 0] + sq[..., 1]).astype(f) + sq[..., 2]).astype(f)
     return np.sqrt(d2).argmin(axis=2)
+
+
+def _fma32(a, b, c):
+    """f32 fma(a, b, c) through float64 (the product of two f32 is exact in float64)."""
+    return (np.float64(a) * np.float64(b) + np.float64(c)).astype(np.float32)
+
+
+def unproject_sum_feature_grad(feat_shape, proj, coords, grad_out, align_corners=False):
+    """d(unproject_heatmaps(..., 'sum'))/d(heatmaps) (op.py:99-163, its autograd through
+    grid_sampler_2d, op.py:134) as the EXACT float64 sum, per heatmap element, of the f32
+    products grad_out * w of every voxel-view tap that reads it, w the forward's own f32
+    bilinear weights: projection as the FMA chain of multiview.py:96, IEEE divisions
+    (multiview.py:75, op.py:128-129), grid_sample's unnormalisation and corner weights
+    (SURVEY.md §8a a1.1-a1.5).  This is what the deterministic backward computes before its
+    final rounding; ATen's sequential float sum on the build container's CPU lies within a
+    few 1e-7 of it."""
+    f32 = np.float32
+    B, N, C, H, W = feat_shape
+    P = np.asarray(proj, np.float32)
+    X = np.asarray(coords, np.float32).reshape(B, -1, 3)
+    G = np.asarray(grad_out, np.float32).reshape(B, C, -1)
+    acc = np.zeros((B, N, C, H, W), np.float64)
+    for b in range(B):
+        x, y, z = X[b, :, 0], X[b, :, 1], X[b, :, 2]
+        for v in range(N):
+            Pv = P[b, v]
+
+            def row(r):
+                t = (np.float64(x) * np.float64(Pv[r, 0])).astype(f32)
+                t = _fma32(y, Pv[r, 1], t)
+                t = _fma32(z, Pv[r, 2], t)
+                return _fma32(f32(1), Pv[r, 3], t)
+            uh, vh, wh = row(0), row(1), row(2)
+            invalid = wh <= 0
+            wh = np.where(wh == 0, f32(1), wh)
+            gx = f32(2) * ((uh / wh).astype(f32) / f32(H) - f32(0.5))
+            gy = f32(2) * ((vh / wh).astype(f32) / f32(W) - f32(0.5))
+            if align_corners:
+                ix = ((gx + f32(1)) * f32((W - 1) * 0.5)).astype(f32)
+                iy = ((gy + f32(1)) * f32((H - 1) * 0.5)).astype(f32)
+            else:
+                ix = _fma32(gx + f32(1), f32(W * 0.5), f32(-0.5))
+                iy = _fma32(gy + f32(1), f32(H * 0.5), f32(-0.5))
+            x0, y0 = np.floor(ix), np.floor(iy)
+            tx, ty = (ix - x0).astype(f32), (iy - y0).astype(f32)
+            sx, sy = f32(1) - tx, f32(1) - ty
+            for wt, dy, dx in ((sy * sx, 0, 0), (sy * tx, 0, 1), (ty * sx, 1, 0), (ty * tx, 1, 1)):
+                xx, yy = x0.astype(np.int64) + dx, y0.astype(np.int64) + dy
+                m = (xx >= 0) & (xx < W) & (yy >= 0) & (yy < H) & ~invalid
+                for c in range(C):
+                    np.add.at(acc[b, v, c], (yy[m], xx[m]),
+                              (G[b, c][m] * wt[m].astype(f32)).astype(f32).astype(np.float64))
+    return acc

@@ -2,7 +2,7 @@
 
 Run in the build container only (it needs /root/reference; the GPU box never runs it):
 
-    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes|ce_loss|v2v_front|chains|dlt_degenerate]   (argument: only that fixture)
+    python -B tests/golden/make_golden.py [softargmax2d|coord_volumes|ce_loss|v2v_front|chains|dlt_degenerate|bwd_elementwise]   (argument: only that fixture)
 
 The reference (learnable-triangulation-pytorch, mvn/utils/op.py and
 mvn/utils/multiview.py) is imported read-only with two in-memory accommodations:
@@ -338,8 +338,36 @@ def golden_dlt_degenerate(multiview):
          out_zero_conf=out_zero_conf.numpy(), out_zero_col=out_zero_col.numpy())
 
 
+def golden_unproject_backward_elementwise(op):
+    """The reference's own autograd gradient of unproject_heatmaps (op.py:99-163: ATen's
+    grid_sampler_2d / softmax backward on THIS host) for the element-wise backward parity
+    test: the upstream gradients span 1e-12 ... 1e8 (frame 1 x 1e8, frame 0 channel 2 x
+    1e-12).  Captured here, with the forward goldens, because ATen's CPU backward is not the
+    same function of its inputs on every host: on the GPU box's EPYC it recomputes the
+    sampling coordinate with a different rounding (profiles/r20_bwd_host_probe_epyc.txt:
+    9.3e-4 element-wise vs 2.9e-7 on this Xeon), so a gradient recomputed there is not the
+    reference's."""
+    vb = synth.volumetric_batch(2, n_views=4, channels=4, heatmap=32, volume=16, seed=8)
+    res = {}
+    gout = torch.rand((2, 4, 16, 16, 16), generator=torch.Generator().manual_seed(6))
+    gout[1] *= 1e8
+    gout[0, 2] *= 1e-12
+    g_sm = torch.randn((2, 4, 16, 16, 16), generator=torch.Generator().manual_seed(7))
+    g_sm[1] *= 1e8
+    for method, feat_scale, g in (("sum", 1.0, gout), ("softmax", 20.0, g_sm)):
+        f = (vb.features * feat_scale).clone().requires_grad_(True)
+        op.unproject_heatmaps(f, vb.proj, vb.coords, method).backward(g)
+        res[f"grad_out_{method}"] = g.numpy()
+        res[f"grad_feat_{method}"] = f.grad.numpy()
+    save("unproject_bwd_elementwise.npz", feat=vb.features.numpy(), proj=vb.proj.numpy(), coords=vb.coords.numpy(),
+         **res)
+
+
 def main():
     op, multiview = import_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "bwd_elementwise":
+        golden_unproject_backward_elementwise(op)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "v2v_front":
         golden_v2v_front()
         return

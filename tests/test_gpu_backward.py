@@ -259,47 +259,40 @@ def test_unproject_backward_nonfinite_follow_the_reference(device, mode, method,
         assert np.isfinite(ours).all()               # the feature gradient does not read feat
 
 
-def test_unproject_backward_fixed_point_keeps_every_element_exact(device):
-    """Per-element precision of the default (fixed-point) backward in one call whose gradients
-    span 1e-12 ... 1e8: frame 1's upstream gradient is 1e8 x frame 0's, and channel 2 of frame
-    0 is another 1e-12 below.  With non-negative upstream gradients and 'sum' aggregation every
-    element is a sum of non-negative f32 products g * w, so a float sum of them is accurate to a
-    few ulps RELATIVE TO THAT ELEMENT; the float-atomic path (LDS ds_add_f32 + global float
-    atomics, same products) is such a sum, and the fixed-point result must match it element by
-    element within 1e-6 relative.  A per-call absolute resolution (round 3's 64-bit format,
-    scaled to the 1e8 frame: unit ~2^-44 of its largest sum) leaves the 1e-12 channel a few
-    bits.  Against the reference's own autograd the comparison is per frame (max_rel): single
-    elements fed only by near-zero tap weights differ by up to ~1e-3 relative, because ATen's
-    backward recomputes the grid coordinate with a different rounding than its forward (ref32
-    vs a float64 re-run differs the same way), so element-wise relative parity with it is not
-    a property of any f32 implementation.  Softmax (coefficients spanning e^-20, both signs)
-    is checked per frame."""
-    from mvn_rocm import synth
-    vb = synth.volumetric_batch(2, n_views=4, channels=4, heatmap=32, volume=16, seed=8)
-    gout = torch.rand((2, 4, 16, 16, 16), generator=torch.Generator().manual_seed(6))
-    gout[1] *= 1e8
-    gout[0, 2] *= 1e-12
-    ours = _grads(device, "sum", vb.features, vb.proj, vb.coords, None, gout, "fixed")[0]
-    flt = _grads(device, "sum", vb.features, vb.proj, vb.coords, None, gout, "float_atomic")[0]
-    ref = _ref_grads("sum", vb.features, vb.proj, vb.coords, None, gout)[0]
-    assert np.array_equal(ours == 0, flt == 0) and np.array_equal(ours == 0, ref == 0)
-    nz = flt != 0
-    rel = np.abs(ours[nz].astype(np.float64) - flt[nz]) / np.abs(flt[nz].astype(np.float64))
-    assert rel.max() <= 1e-6, rel.max()
-    for b in range(2):
-        assert max_rel(ours[b], ref[b]) <= 1e-5
-    assert max_rel(ours[0, :, 2], ref[0, :, 2]) <= 1e-5           # the 1e-12 channel on its own
+def test_unproject_backward_fixed_point_keeps_every_element_exact(golden, device):
+    """Per-element parity of the default (fixed-point) backward with the reference's own
+    autograd in one call whose gradients span 1e-12 ... 1e8: frame 1's upstream gradient is
+    1e8 x frame 0's, and channel 2 of frame 0 is another 1e-12 below.  The reference gradient
+    is the golden captured from mvn/utils/op.py's autograd in the build container
+    (tests/golden/unproject_bwd_elementwise.npz), not recomputed here: ATen's CPU
+    grid_sampler backward is host-dependent — on this box's EPYC it recomputes the sampling
+    coordinate with a different rounding than its forward and differs from the container's
+    Xeon result by up to 9.3e-4 element-wise (profiles/r20_bwd_host_probe_epyc.txt), while the
+    Xeon result is the exact sum of the forward's own tap products to 2.9e-7.
+      'sum' (non-negative upstream gradient): EVERY nonzero element within 1e-5 relative of the
+        reference, zeros at exactly the reference's zeros; the float-atomic path (same
+        products, float sums) agrees with the fixed-point one within 1e-6 per element.
+      'softmax' (sharpened features, both signs; coefficients spanning e^-20): per frame
+        within 5e-5 of the reference (its own f32 gradient is 1.6e-5 / 2.3e-5 from its float64
+        re-run)."""
+    d = golden("unproject_bwd_elementwise.npz")
+    feat, P, coords = (torch.from_numpy(d[k]) for k in ("feat", "proj", "coords"))
+    gout = torch.from_numpy(d["grad_out_sum"])
+    ref = d["grad_feat_sum"]
+    ours = _grads(device, "sum", feat, P, coords, None, gout, "fixed")[0]
+    flt = _grads(device, "sum", feat, P, coords, None, gout, "float_atomic")[0]
+    assert np.array_equal(ours == 0, ref == 0) and np.array_equal(flt == 0, ref == 0)
+    nz = ref != 0
+    rel = np.abs(ours[nz].astype(np.float64) - ref[nz]) / np.abs(ref[nz].astype(np.float64))
+    assert rel.max() <= 1e-5, rel.max()
+    rel_f = np.abs(ours[nz].astype(np.float64) - flt[nz]) / np.abs(flt[nz].astype(np.float64))
+    assert rel_f.max() <= 1e-6, rel_f.max()
     # the two frames and the tiny channel each really are at their own scale
     assert np.abs(ref[1]).max() > 1e6 * np.abs(ref[0]).max() > 0
     assert 0 < np.abs(ref[0, :, 2]).max() < 1e-10 * np.abs(ref[0]).max()
 
-    feat = vb.features * 20.0                        # sharply peaked view weights
-    g = torch.randn((2, 4, 16, 16, 16), generator=torch.Generator().manual_seed(7))
-    g[1] *= 1e8
-    ours = _grads(device, "softmax", feat, vb.proj, vb.coords, None, g, "fixed")[0]
-    ref = _ref_grads("softmax", feat, vb.proj, vb.coords, None, g)[0]
-    # at these sharpened features the reference's own f32 gradient is 1.6e-5 / 2.3e-5 (per
-    # frame) from its float64 re-run; 5e-5 keeps the per-frame bar at twice that
+    ours = _grads(device, "softmax", feat * 20.0, P, coords, None, torch.from_numpy(d["grad_out_softmax"]), "fixed")[0]
+    ref = d["grad_feat_softmax"]
     for b in range(2):
         assert np.abs(ref[b]).max() > 0
         assert max_rel(ours[b], ref[b]) <= 5e-5

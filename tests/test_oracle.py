@@ -295,3 +295,17 @@ def test_c_oracle_nan_features_follow_torch(golden, method):
                                            torch.from_numpy(d["coords"]), method, torch.from_numpy(d["conf"])).numpy()
     assert np.isnan(ref).sum() > 50
     assert_parity_with_nans(out, ref, method, tol=1e-6)
+
+
+def test_backward_golden_is_the_exact_sum_of_forward_tap_products(golden):
+    """The element-wise backward golden (the reference's own autograd, captured in the build
+    container) equals the exact sum of the forward's f32 tap products per element within
+    1e-6 relative: the reference's 'sum' feature gradient on that host is that sum, which is
+    what the GPU's deterministic backward is checked to reproduce (test_gpu_backward.py)."""
+    from oracle import restate_np
+    d = golden("unproject_bwd_elementwise.npz")
+    ref = d["grad_feat_sum"].astype(np.float64)
+    ex = restate_np.unproject_sum_feature_grad(d["feat"].shape, d["proj"], d["coords"], d["grad_out_sum"])
+    assert np.array_equal(ex == 0, ref == 0)
+    nz = ref != 0
+    assert (np.abs(ex[nz] - ref[nz]) / np.abs(ref[nz])).max() <= 1e-6

@@ -119,11 +119,17 @@ __device__ __forceinline__ void wave_merge(float& m, float& s, float& sx, float&
 template <int CTRL, int RMASK> __device__ __forceinline__ float dpp_f(float v, float ident) {
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(ident), __float_as_int(v), CTRL, RMASK, 0xf, false));
 }
+// (the max written as DPP-fused v_max_f32 with dst == src1: a lane without a source is
+// disabled and keeps its value; through fmaxf every DPP result was canonicalised first)
 __device__ __forceinline__ float wave_max63(float v) {
-  constexpr float I = -INFINITY;
-  v = fmaxf(v, dpp_f<0x111, 0xf>(v, I)); v = fmaxf(v, dpp_f<0x112, 0xf>(v, I));
-  v = fmaxf(v, dpp_f<0x114, 0xf>(v, I)); v = fmaxf(v, dpp_f<0x118, 0xf>(v, I));
-  v = fmaxf(v, dpp_f<0x142, 0xa>(v, I)); v = fmaxf(v, dpp_f<0x143, 0xc>(v, I));
+  asm("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "s_nop 1"
+      : "+v"(v));
   return v;
 }
 __device__ __forceinline__ float wave_sum63(float v) {
@@ -131,6 +137,34 @@ __device__ __forceinline__ float wave_sum63(float v) {
   v += dpp_f<0x114, 0xf>(v, 0.f); v += dpp_f<0x118, 0xf>(v, 0.f);
   v += dpp_f<0x142, 0xa>(v, 0.f); v += dpp_f<0x143, 0xc>(v, 0.f);
   return v;
+}
+
+// Max of a lane's values as a tree of three-operand maxima: 8 v_max3_f32 for 16 values.
+// (fmaxf on the raw loaded values would first canonicalise each input — one more v_max per
+// value in IEEE mode — so the instruction is written out.  NaNs are dropped as fmaxf does.)
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// level by level: groups of three, a leftover pair or single carried up
+template <int N>
+__device__ __forceinline__ float max_level(const float* v) {
+  if constexpr (N == 1) {
+    return v[0];
+  } else {
+    constexpr int M = (N + 2) / 3;
+    float w[M];
+#pragma unroll
+    for (int i = 0; i < N / 3; ++i) w[i] = vmax3(v[3 * i], v[3 * i + 1], v[3 * i + 2]);
+    if constexpr (N % 3 == 2) w[M - 1] = vmax3(v[N - 2], v[N - 1], v[N - 1]);
+    if constexpr (N % 3 == 1) w[M - 1] = v[N - 1];
+    return max_level<M>(w);
+  }
+}
+template <int R, int V>
+__device__ __forceinline__ float max_tree(const float (&x)[R][V]) {
+  return max_level<R * V>(&x[0][0]);
 }
 
 // Pass 1: one WAVE per (frame, 512-voxel chunk), looping over ALL joints — no barriers,
@@ -207,11 +241,14 @@ __global__ __launch_bounds__(kSaBlock) void softargmax_partials(
     float m = 0.f, s = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
     if constexpr (SOFTMAX) {
       constexpr float kLog2e = 1.4426950408889634f;
-      float lm = -INFINITY;
+      // x * 1 == x: the reference's models use volume_multiplier 1.0 (a scalar branch)
+      if (mult != 1.f) {
 #pragma unroll
-      for (int r = 0; r < RUNS; ++r)
+        for (int r = 0; r < RUNS; ++r)
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) { x[r][k] = x[r][k] * mult; lm = fmaxf(lm, x[r][k]); }
+          for (int k = 0; k < VEC; ++k) x[r][k] = x[r][k] * mult;
+      }
+      const float lm = max_tree(x);
       m = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wave_max63(lm)), kWave - 1));
       if (m != -INFINITY) {                            // wave-uniform
         const float ml = m * kLog2e;

@@ -210,21 +210,34 @@ def telemetry(device, step, seconds=0.06, samples=6):
         step(False)
     reads = {"sclk_mhz": [], "mclk_mhz": [], "power_w": [], "temp_hotspot_c": [], "gfx_activity_pct": [],
              "throttle_status": []}
+
+    def num(d, *keys):              # the first numeric field ("N/A" strings are skipped)
+        for k in keys:
+            if isinstance(d.get(k), (int, float)):
+                return d[k]
+        return None
+    m0 = _smi(amdsmi.amdsmi_get_gpu_metrics_info, h) or {}
     for _ in range(samples):
         time.sleep(seconds / (2 * samples))
         g = _smi(amdsmi.amdsmi_get_clock_info, h, amdsmi.AmdSmiClkType.GFX) or {}
         m = _smi(amdsmi.amdsmi_get_clock_info, h, amdsmi.AmdSmiClkType.MEM) or {}
         pw = _smi(amdsmi.amdsmi_get_power_info, h) or {}
         mt = _smi(amdsmi.amdsmi_get_gpu_metrics_info, h) or {}
-        for k, v in (("sclk_mhz", g.get("clk", g.get("cur_clk"))), ("mclk_mhz", m.get("clk", m.get("cur_clk"))),
-                     ("power_w", pw.get("average_socket_power", pw.get("current_socket_power"))),
-                     ("temp_hotspot_c", mt.get("temperature_hotspot")), ("gfx_activity_pct", mt.get("average_gfx_activity")),
-                     ("throttle_status", mt.get("throttle_status"))):
+        for k, v in (("sclk_mhz", num(g, "clk", "cur_clk")), ("mclk_mhz", num(m, "clk", "cur_clk")),
+                     ("power_w", num(pw, "current_socket_power", "socket_power", "average_socket_power")),
+                     ("temp_hotspot_c", num(mt, "temperature_hotspot")), ("gfx_activity_pct", num(mt, "average_gfx_activity")),
+                     ("throttle_status", num(mt, "throttle_status"))):
             if isinstance(v, (int, float)):
                 reads[k].append(v)
+    m1 = _smi(amdsmi.amdsmi_get_gpu_metrics_info, h) or {}
     torch.cuda.synchronize()
     out = {k: (statistics.median(v) if v else None) for k, v in reads.items()}
     out["samples"] = samples
+    # share of the sampling window the SMU spent at the package power limit (PPT residency
+    # accumulator over the firmware's accumulation counter; 0 = never power-limited)
+    dp, da = (num(m1, "ppt_residency_acc") or 0) - (num(m0, "ppt_residency_acc") or 0), \
+        (num(m1, "accumulation_counter") or 0) - (num(m0, "accumulation_counter") or 0)
+    out["ppt_limited_frac"] = round(dp / da, 4) if da > 0 else None
     return out
 
 

@@ -301,8 +301,10 @@ def copy_bandwidth(device):
         src = torch.empty(n, device=device).normal_()
         dst = torch.empty_like(src)
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < 0.3:
-            dst.copy_(src)
+        while time.perf_counter() - t0 < 0.3:     # (synchronised: enqueueing alone queued ~1.5 s of copies)
+            for _ in range(4):
+                dst.copy_(src)
+            torch.cuda.synchronize()
         best = float("inf")
         for _ in range(3):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -463,7 +463,12 @@ def run_config5(args, rank, world, device, clock, cuboid=False):
                 roofline={"kernel": "v2v_front<bf16> (Conv3d 32->16 k7 + BN + ReLU)", "bound": "mfma",
                           "achieved": tflops, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": tflops / MFMA_BF16_PEAK_TFLOPS, "launch_ms": conv_ms,
-                          "flop_per_launch": V2V_FLOP_PER_FRAME * B})
+                          "flop_per_launch": V2V_FLOP_PER_FRAME * B,
+                          # the dense peak is quoted at 2.4 GHz; bf16 MFMA loads hold a lower
+                          # clock (MI355X_MICROARCH.md 'DVFS give-back'): the fraction of the
+                          # peak at the sclk this config held (telemetry), an MFMA-pipe figure
+                          "frac_at_held_clock": (tflops / (MFMA_BF16_PEAK_TFLOPS * tel["sclk_mhz"] / 2400.0)
+                                                 if tel and tel.get("sclk_mhz") else None)})
 
 
 def run_config1(args, device):

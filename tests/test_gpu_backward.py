@@ -259,6 +259,38 @@ def test_unproject_backward_nonfinite_follow_the_reference(device, mode, method,
         assert np.isfinite(ours).all()               # the feature gradient does not read feat
 
 
+@pytest.mark.parametrize("mode", ("fixed", "float_atomic"))
+@pytest.mark.parametrize("method", ("softmax", "conf"))
+@pytest.mark.parametrize("what", ("feat_inf", "conf_inf"))
+def test_unproject_backward_direct_path_partial_tiles_nonfinite(device, mode, method, what):
+    """The global-atomic path (footprints past the LDS budget: 96^2 maps on a coarse 13^3 grid)
+    on partial tiles (13 is no multiple of the tile): threads past the volume's edge scatter
+    nothing, so an infinite confidence or feature produces +-inf exactly where the reference's
+    autograd does and no NaN at voxel 0's taps."""
+    from mvn_rocm import synth
+    if what == "conf_inf" and method != "conf":
+        pytest.skip("confidences only enter conf*")
+    vb = synth.volumetric_batch(2, n_views=4, channels=4, heatmap=96, volume=13, seed=8)
+    feat, P, coords = vb.features.clone(), vb.proj, vb.coords
+    conf = torch.from_numpy(np.random.default_rng(8).uniform(0.2, 1.0, (2, 4, 4)).astype(np.float32)) \
+        if method == "conf" else None
+    gout = torch.randn((2, 4, 13, 13, 13), generator=torch.Generator().manual_seed(9))
+    if what == "feat_inf":
+        feat[0, 2, 1, 48, 47] = float("inf")
+        feat[1, 0, 3, 47, 48] = -float("inf")
+    else:
+        conf[0, 1, 2] = float("inf")
+    ours, ours_c = _grads(device, method, feat, P, coords, conf, gout, mode)
+    ref, ref_c = _ref_grads(method, feat, P, coords, conf, gout)
+    assert not (np.isfinite(ref).all() and (ref_c is None or np.isfinite(ref_c).all()))   # the input reached
+    _same_nonfinite(ours, ref)
+    fin = np.isfinite(ref)
+    assert fin.any()
+    assert max_rel(ours[fin], ref[fin]) <= 5e-5          # atomic summation order
+    if method == "conf":
+        _same_nonfinite(ours_c, ref_c)
+
+
 def test_unproject_backward_fixed_point_keeps_every_element_exact(golden, device):
     """Per-element parity of the default (fixed-point) backward with the reference's own
     autograd in one call whose gradients span 1e-12 ... 1e8: frame 1's upstream gradient is

@@ -105,8 +105,9 @@ def launch_ranks(n: int) -> int:
 class Clock:
     """Barrier + device sync around the timed region; max over ranks."""
 
-    def __init__(self, world, device, dry):
+    def __init__(self, world, device, dry, host_collectives=False):
         self.world, self.device, self.dry = world, device, dry
+        self.host = host_collectives       # gloo process group: collectives on host tensors
 
     def sync(self):
         import torch
@@ -125,7 +126,7 @@ class Clock:
         import torch.distributed as dist
         if self.world == 1:
             return seconds
-        t = torch.tensor([seconds], device=self.device, dtype=torch.float64)
+        t = torch.tensor([seconds], device="cpu" if self.host else self.device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -334,12 +335,14 @@ def roofline(c, r, cfg_name, device=None):
 class Workload:
     """One rank's frames of a config, resident on the device, and the timed step."""
 
-    def __init__(self, cfg, rank, world, device, seed=0, cuboid=False, first_frame=None):
+    def __init__(self, cfg, rank, world, device, seed=0, cuboid=False, first_frame=None, global_batch=None):
         import torch
         from mvn_rocm import synth
         self.cfg, self.world, self.device = cfg, world, device
         B = cfg["frames"]
-        self.global_batch = B * world
+        # ragged strong-scaling shards (config 4 over N not dividing 128): the caller passes the
+        # true global batch, or ranks would pad the joints all-gather to different sizes
+        self.global_batch = B * world if global_batch is None else global_batch
         first = rank * B if first_frame is None else first_frame
         vb = synth.volumetric_batch(B, n_views=cfg["views"], channels=cfg["channels"], heatmap=cfg["heatmap"],
                                     volume=cfg["volume"], dtype=cfg["dtype"], device=device, seed=seed,
@@ -392,10 +395,11 @@ class Workload:
         return (sum(a.elapsed_time(b) for a, b, _ in self.ev) / n, sum(b.elapsed_time(c) for _, b, c in self.ev) / n)
 
 
-def run_config(name, args, rank, world, device, clock, cuboid=False, cfg=None, first_frame=None, starts=None):
+def run_config(name, args, rank, world, device, clock, cuboid=False, cfg=None, first_frame=None, starts=None,
+               global_batch=None):
     import torch
     cfg = cfg if cfg is not None else _configs()[name]
-    wl = Workload(cfg, rank, world, device, cuboid=cuboid, first_frame=first_frame)
+    wl = Workload(cfg, rank, world, device, cuboid=cuboid, first_frame=first_frame, global_batch=global_batch)
     wl.starts = starts if starts is not None else [r * cfg["frames"] for r in range(world)]
     wl.reserve_events(args.steps)
     elapsed = timed_loop(lambda t: wl.step(t), args, clock)
@@ -752,6 +756,11 @@ def main():
     ap.add_argument("--no-in-kernel-coords", action="store_true",
                     help="skip the in-kernel-coordinates run (keeps rocprof kernel means per variant clean)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo protocol check, no GPU")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="(tests) gloo runs the multi-rank protocol with host-side collectives, e.g. several "
+                         "ranks sharing one GPU (RCCL refuses two ranks on one device)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="(tests, with --dist-backend gloo) every rank computes on cuda:0")
     ap.add_argument("--dry-run-fail-rank", type=int, default=-1,
                     help="(tests) this rank of a dry run exits with an error before its first barrier")
     args = ap.parse_args()
@@ -781,11 +790,18 @@ def main():
             dist.destroy_process_group()
         return
 
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    if args.share_device and args.dist_backend != "gloo":
+        raise SystemExit("--share-device needs --dist-backend gloo (RCCL refuses two ranks on one GPU)")
+    device = torch.device("cuda", 0 if args.share_device else local)
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
-    clock = Clock(world, device, False)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
+    clock = Clock(world, device, False, host_collectives=args.dist_backend == "gloo")
+    coll = (f"all_gather joints ({'RCCL' if args.dist_backend == 'nccl' else 'gloo, host tensors'})"
+            if world > 1 else None)
     configs = _configs()
     extras = not args.no_secondary and args.config == "2"
 
@@ -815,12 +831,12 @@ def main():
         start, count = mdist.shard(128, world, rank)
         c4 = dict(configs["4"], frames=count)
         r4 = run_config("4", args, rank, world, device, clock, cfg=c4, first_frame=start,
-                        starts=[mdist.shard(128, world, q)[0] for q in range(world)])
+                        starts=[mdist.shard(128, world, q)[0] for q in range(world)], global_batch=128)
         cfg4 = dict(workload=c4["label"] + ", global batch 128 split over the ranks", value=128 * args.steps / r4["elapsed"],
                     unit="frames/s", scaling="strong", global_batch=128, frames_per_gpu=count,
                     ms_per_step=r4["ms_per_step"], unproject_ms=r4["unproject_ms"],
                     unproject_achieved_gbps=r4["achieved_gbps"], unproject_frac=r4["achieved_gbps"] / HBM_PEAK_GBPS,
-                    collective="all_gather joints (RCCL)" if world > 1 else None, telemetry=r4["telemetry"])
+                    collective=coll, telemetry=r4["telemetry"])
         cfg5 = run_config5(args, rank, world, device, clock)
         if not args.no_in_kernel_coords:
             k5 = run_config5(args, rank, world, device, clock, cuboid=True)
@@ -866,7 +882,7 @@ def main():
             "config": {"workload": c["label"], "global_batch": c["frames"] * world, "frames_per_gpu": c["frames"],
                        "views": c["views"], "channels": c["channels"], "heatmap": c["heatmap"],
                        "volume": c["volume"], "joints": c["joints"], "parallelism": f"dp{world}",
-                       "collective": "all_gather joints (RCCL)" if world > 1 else None},
+                       "collective": coll, **({"device_shared": True} if args.share_device else {})},
             "roofline": roofline(c, r, args.config, device),
             "softargmax_ms": r["softargmax_ms"],
             "path_algorithmic_gbps": r["path_gbps"],

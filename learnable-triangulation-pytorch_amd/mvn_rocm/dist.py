@@ -32,6 +32,9 @@ def gather_joints(local: torch.Tensor, global_batch: int, group=None) -> torch.T
     world = dist.get_world_size(group)
     if world == 1:
         return local
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo collectives take host tensors (tests: several ranks sharing one GPU)
+        return gather_joints(local.cpu(), global_batch, group).to(local.device)
     per = -(-global_batch // world)
     J = local.shape[1]
     send = local.new_zeros((per, J, 3))

@@ -189,7 +189,7 @@ def gpu_identity(device):
             "market_name": asic.get("market_name"), "power_cap_w": (cap.get("power_cap") or 0) / 1e6 or None}
 
 
-def telemetry(device, step, seconds=0.06, samples=6):
+def telemetry(device, step, seconds=0.15, samples=6):
     """Clocks, power and temperature the GPU holds under this config's load: an untimed burst
     of the same step (~`seconds` of GPU work, right after the timed region, so the same
     thermal and power state) is enqueued and amdsmi is sampled while it runs.  Medians of
@@ -204,9 +204,10 @@ def telemetry(device, step, seconds=0.06, samples=6):
         return None
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    step(False)
+    for _ in range(10):         # GPU time per step (one synchronised step would count the sync)
+        step(False)
     torch.cuda.synchronize()
-    per = max(time.perf_counter() - t0, 1e-5)
+    per = max((time.perf_counter() - t0) / 10, 1e-5)
     for _ in range(max(4, int(seconds / per))):
         step(False)
     reads = {"sclk_mhz": [], "mclk_mhz": [], "power_w": [], "temp_hotspot_c": [], "gfx_activity_pct": [],

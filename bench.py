@@ -20,7 +20,13 @@ ranks).  Rank 0 prints ONE JSON line.
 
 --dry-run runs the whole multi-process protocol on the CPU (gloo): rank bring-up,
 barriers, max-over-ranks timing and the joints all-gather, with a stand-in step that
-needs no GPU (tests/test_bench.py).
+needs no GPU (tests/test_bench.py).  --dist-backend gloo --share-device runs the real GPU
+step on several ranks sharing cuda:0 with host-side collectives (RCCL refuses two ranks on
+one device): the multi-rank path on a one-GPU box (tests/test_gpu_bench_multirank.py).
+
+Every config also reports `telemetry` (sclk, mclk, socket power, hotspot temperature, GFX
+activity and power-limit residency sampled during an untimed burst of the same step right
+after its timed region) and the line carries `gpu` (UUID, ASIC serial, power cap).
 
 With the default --config 2 the line also carries `secondary` (config 3, bf16, 32 frames,
 with its own roofline block), `config1` (the algebraic path: DLT at batch 1, 4 views x 17

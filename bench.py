@@ -249,6 +249,40 @@ def telemetry(device, step, seconds=0.15, samples=6):
     return out
 
 
+def rank_identity(device, rank, local, dry):
+    """Who this rank is and which device it computed on: (rank, local rank, host, pid) and the
+    device's UUID (amdsmi, else torch's), PCI address and name.  Gathered from every rank, the
+    list shows that an N-rank RCCL line ran on N distinct GPUs."""
+    ident = {"rank": rank, "local_rank": local, "host": socket.gethostname(), "pid": os.getpid()}
+    if dry:
+        ident.update(device="cpu", device_uuid=None)
+        return ident
+    import torch
+    p = torch.cuda.get_device_properties(device)
+    g = gpu_identity(device) or {}
+    ident.update(device=str(device), device_uuid=g.get("uuid") or str(getattr(p, "uuid", "")) or None,
+                 pci=f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", name=p.name)
+    return ident
+
+
+def gather_objects(obj, world):
+    """[obj of rank 0, ..., obj of rank world-1] on every rank (one all_gather_object)."""
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def dist_record(ident, world, backend):
+    """The line's `dist` block: backend, every rank's identity, and the number of distinct
+    devices they computed on (== world under RCCL, which refuses two ranks on one GPU)."""
+    ranks = gather_objects(ident, world)
+    devs = {(r["host"], r.get("device_uuid") or r.get("pci") or r["device"]) for r in ranks}
+    return {"backend": backend, "world": world, "ranks": ranks, "distinct_devices": len(devs)}
+
+
 # ----------------------------------------------------------------------------- algorithmic bytes
 def unproject_bytes(c, E, cuboid=False):
     """Algorithmic bytes of one frame's unprojection: features read once,
@@ -267,7 +301,7 @@ def frame_bytes(c, E, cuboid=False):
             + coords + 4 * (12 * c["views"] + 3 * c["joints"]))
 
 
-def measured_traffic(cfg_name):
+def measured_traffic(cfg_name, precision="exact"):
     """HBM bytes per unprojection launch from the newest committed PMC summary
     (profiles/rNN_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the
     same kernel and config), or None."""
@@ -277,17 +311,25 @@ def measured_traffic(cfg_name):
         return None, None
     data = json.load(open(files[-1]))
     for k, d in data.get(f"cfg{cfg_name}", {}).items():
-        if k.startswith(("unproject_x4<2,", "unproject_tiled<2,")) and "hbm_bytes_per_launch" in d:
+        if not (k.startswith(("unproject_x4<2,", "unproject_tiled<2,")) and "hbm_bytes_per_launch" in d):
+            continue
+        # unproject_x4<AGG, TIn, TOut, K, CL, FAST>: the last template argument is the arithmetic
+        # (profiles before round 6 name 5 arguments: exact)
+        args = k[k.index("<") + 1:k.rindex(">")].split(",")
+        fast = k.startswith("unproject_x4") and len(args) >= 6 and args[5].strip() == "1"
+        if fast == (precision == "fast"):
             return d["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
     return None, None
 
 
-def kernel_name(c):
+def kernel_name(c, precision="exact"):
     import torch
     t = "float" if c["dtype"] == torch.float32 else "bf16"
+    p = "" if precision == "exact" else (", fast: bf16 pixel-pair slots, v_dot2" if t == "bf16" and c["views"] == 4
+                                        else ", fast")
     if c["views"] == 4:      # the chunk-staged kernel (csrc/unproject_x4.hip), tile per dtype
-        return f"unproject_x4<softmax, {t}, {t}, tile {'4x8x16' if t == 'float' else '4x8x8'}>"
-    return f"unproject_x4<softmax, {t}, {t}, 8 views, 2-channel slots, tile 4x8x8>"
+        return f"unproject_x4<softmax, {t}, {t}, tile {'4x8x16' if t == 'float' else '4x8x8'}{p}>"
+    return f"unproject_x4<softmax, {t}, {t}, 8 views, 2-channel slots, tile 4x8x8{p}>"
 
 
 def dtype_name(dt):
@@ -328,8 +370,9 @@ def copy_bandwidth(device):
 
 
 def roofline(c, r, cfg_name, device=None):
-    traffic, src = measured_traffic(cfg_name)
-    out = {"kernel": kernel_name(c), "bound": "hbm", "achieved": r["achieved_gbps"], "peak": HBM_PEAK_GBPS,
+    prec = r.get("precision", "exact")
+    traffic, src = measured_traffic(cfg_name, prec)
+    out = {"kernel": kernel_name(c, prec), "precision": prec, "bound": "hbm", "achieved": r["achieved_gbps"], "peak": HBM_PEAK_GBPS,
            "unit": "GB/s", "frac": r["achieved_gbps"] / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": src,
            "launch_ms": r["unproject_ms"], "algorithmic_bytes_per_launch": r["launch_bytes"]}
     if device is not None:
@@ -342,10 +385,12 @@ def roofline(c, r, cfg_name, device=None):
 class Workload:
     """One rank's frames of a config, resident on the device, and the timed step."""
 
-    def __init__(self, cfg, rank, world, device, seed=0, cuboid=False, first_frame=None, global_batch=None):
+    def __init__(self, cfg, rank, world, device, seed=0, cuboid=False, first_frame=None, global_batch=None,
+                 precision="exact"):
         import torch
         from mvn_rocm import synth
         self.cfg, self.world, self.device = cfg, world, device
+        self.precision = precision      # the unprojection's arithmetic (DESIGN.md §4.1a)
         B = cfg["frames"]
         # ragged strong-scaling shards (config 4 over N not dividing 128): the caller passes the
         # true global batch, or ranks would pad the joints all-gather to different sizes
@@ -376,13 +421,13 @@ class Workload:
         torch.cuda.synchronize()
         self.ev = []
 
-    def step(self, timed=False):
+    def step(self, timed=False, gather=True):
         from mvn_rocm import dist as mdist, op
         J = self.cfg["joints"]
         if timed:
             e0, e1, e2 = self._pool[len(self.ev)]
             e0.record()
-        vol = op.unproject_heatmaps(self.feat, self.proj, self.coords, "softmax")
+        vol = op.unproject_heatmaps(self.feat, self.proj, self.coords, "softmax", precision=self.precision)
         if timed:
             e1.record()
         xyz, sm = op.integrate_tensor_3d_with_coordinates(vol[:, :J], self.coords, True)
@@ -390,7 +435,7 @@ class Workload:
             e2.record()
             self.ev.append((e0, e1, e2))
         self.last = (vol, xyz)
-        if self.world > 1:      # the path's one exchange: joints of every rank, RCCL over xGMI
+        if self.world > 1 and gather:   # the path's one exchange: joints of every rank, RCCL over xGMI
             xyz = mdist.gather_joints(xyz, self.global_batch)
             self.gathered = xyz
         return xyz, sm
@@ -403,19 +448,24 @@ class Workload:
 
 
 def run_config(name, args, rank, world, device, clock, cuboid=False, cfg=None, first_frame=None, starts=None,
-               global_batch=None):
+               global_batch=None, precision=None):
     import torch
     cfg = cfg if cfg is not None else _configs()[name]
-    wl = Workload(cfg, rank, world, device, cuboid=cuboid, first_frame=first_frame, global_batch=global_batch)
+    precision = precision or args.precision
+    wl = Workload(cfg, rank, world, device, cuboid=cuboid, first_frame=first_frame, global_batch=global_batch,
+                  precision=precision)
     wl.starts = starts if starts is not None else [r * cfg["frames"] for r in range(world)]
     wl.reserve_events(args.steps)
     elapsed = timed_loop(lambda t: wl.step(t), args, clock)
     E = 2 if cfg["dtype"] == torch.bfloat16 else 4
     frames_total = wl.global_batch * args.steps
     unproj_ms, sa_ms = wl.kernel_ms()
-    tel = telemetry(device, lambda t: wl.step(t)) if world == 1 else None
+    # every rank samples its own GPU (the line carries the per-rank list at world > 1); the burst
+    # runs each rank's local step only — a rank-dependent count of collectives would deadlock
+    tel = telemetry(device, lambda t: wl.step(t, gather=False))
     launch_bytes = unproject_bytes(cfg, E, cuboid) * cfg["frames"]
-    return dict(cfg=cfg, workload=wl, elapsed=elapsed, fps=frames_total / elapsed, ms_per_step=elapsed / args.steps * 1e3,
+    return dict(cfg=cfg, workload=wl, precision=precision, elapsed=elapsed, fps=frames_total / elapsed,
+                ms_per_step=elapsed / args.steps * 1e3,
                 unproject_ms=unproj_ms, softargmax_ms=sa_ms, launch_bytes=launch_bytes,
                 achieved_gbps=launch_bytes / (unproj_ms * 1e-3) / 1e9,
                 path_gbps=frame_bytes(cfg, E, cuboid) * frames_total / elapsed / 1e9, telemetry=tel)
@@ -459,7 +509,7 @@ def run_config5(args, rank, world, device, clock, cuboid=False):
 
     elapsed = timed_loop(step, args, clock)
     conv_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
-    tel = telemetry(device, step) if world == 1 else None
+    tel = telemetry(device, step)
     tflops = V2V_FLOP_PER_FRAME * B / (conv_ms * 1e-3) / 1e12
     # the same work through the one-call pipeline (mvn_unproject_v2v_front: frame groups of 8
     # through a 134 MB workspace instead of the 1.07 GB whole-batch intermediate)
@@ -619,7 +669,13 @@ def _np_feat(t):
     return t.view(torch.int16).numpy().view(np.uint16) if t.dtype == torch.bfloat16 else t.numpy()
 
 
-def parity_unproject(feat, proj, coords, vol, J, frames, xyz=None, layout="ncdhw"):
+def _within_fast_bar(got, ref):
+    """The fast mode's bar for a bf16 volume: one bf16 ulp of the f32
+    oracle + 2^-8 x max|ref| (bf16 bilinear weights)."""
+    return _within_one_bf16_ulp(got, ref, 2.0 ** -8)
+
+
+def parity_unproject(feat, proj, coords, vol, J, frames, xyz=None, layout="ncdhw", precision="exact"):
     """Frames `frames` of a timed unprojection (softmax agg) against the C oracle
     (oracle/mvn_oracle.c, pinned to the reference's goldens) on the same inputs.
       unproject_max_rel    GPU volume vs oracle unproject_heatmaps (op.py:99-163):
@@ -643,9 +699,12 @@ def parity_unproject(feat, proj, coords, vol, J, frames, xyz=None, layout="ncdhw
             got = got.permute(0, 4, 1, 2, 3)
         got_vol = got.float().cpu().numpy()
         out["unproject_max_rel"] = max(out["unproject_max_rel"], _rel(got_vol, ref_vol))
-        if vol.dtype == torch.bfloat16:
+        if vol.dtype == torch.bfloat16 and precision == "exact":
             ok = _within_one_bf16_ulp(got_vol, ref_vol, 1e-5)
             out["unproject_within_one_bf16_ulp"] = out.get("unproject_within_one_bf16_ulp", True) and ok
+        elif vol.dtype == torch.bfloat16:
+            ok = _within_fast_bar(got_vol, ref_vol)
+            out["unproject_within_fast_bar"] = out.get("unproject_within_fast_bar", True) and ok
         if xyz is not None:
             got_xyz = xyz[f:f + 1].cpu().numpy().astype(np.float64)
             own_xyz, _ = capi.softargmax3d(np.ascontiguousarray(got_vol[:, :J]), co, True, 1.0)
@@ -663,9 +722,14 @@ def parity_check(res):
     wl = res["workload"]
     vol, xyz = wl.last
     t0 = time.perf_counter()
-    out = parity_unproject(wl.feat, wl.proj, wl.coords, vol, wl.cfg["joints"], _frames(vol.shape[0]), xyz)
-    return dict(out, bars="unproject <= 1e-5 (f32 out) / one bf16 ulp (bf16 out); joints <= 1e-4 (north_star)",
-                oracle="oracle/mvn_oracle.c via oracle/capi.py", oracle_s=time.perf_counter() - t0)
+    out = parity_unproject(wl.feat, wl.proj, wl.coords, vol, wl.cfg["joints"], _frames(vol.shape[0]), xyz,
+                           precision=wl.precision)
+    bars = ("unproject <= 1e-5 (f32 out) / one bf16 ulp (bf16 out); joints <= 1e-4 (north_star)"
+            if wl.precision == "exact" else
+            "fast mode: unproject <= 1e-5 (f32 maps) / one bf16 ulp + 2^-8 max|ref| (bf16 maps); chain joints <= 1e-4 "
+            "(north_star)")
+    return dict(out, precision=wl.precision, bars=bars, oracle="oracle/mvn_oracle.c via oracle/capi.py",
+                oracle_s=time.perf_counter() - t0)
 
 
 def parity_check5(r5):
@@ -720,10 +784,14 @@ def verify_gather(res):
 # ----------------------------------------------------------------------------- dry run (CPU)
 def dry_run(args, rank, world):
     """The multi-rank protocol of the bench on the CPU (gloo): every rank builds its own
-    frames of a miniature config-2 batch from (seed, global frame index), a stand-in step
-    (the mean of each frame's coordinate volume as 17 'joints') and the joints all-gather;
-    rank 0 checks the gathered joints against all frames built locally."""
+    frames from (seed, global frame index), a stand-in step (the mean of each frame's
+    coordinate volume as 17 'joints') and the joints all-gather; rank 0 checks the gathered
+    joints against all frames built locally.  Two legs, as the GPU line: config 2's weak
+    scaling (8 frames per rank) and config 4's strong scaling (a global batch of 128 split
+    over the ranks, ragged when the world does not divide it).  The line carries the same
+    `dist` block (backend, every rank's identity) as a GPU line."""
     import torch
+    import torch.distributed as dist
     from mvn_rocm import dist as mdist, synth
     B = 8
     G = B * world
@@ -741,12 +809,35 @@ def dry_run(args, rank, world):
     elapsed = timed_loop(step, args, clock)
     got = step(False)
     ok = bool(torch.equal(got, joints(0, G))) if rank == 0 else None
+
+    # config 4's shape: 128 frames split over the ranks
+    G4 = 128
+    start, count = mdist.shard(G4, world, rank)
+    local4 = joints(start, count)
+
+    def step4(_timed):
+        return mdist.gather_joints(local4, G4) if world > 1 else local4
+
+    el4 = timed_loop(step4, args, clock)
+    got4 = step4(False)
+    shards = gather_objects([start, count], world)
+    ok4 = None
+    if rank == 0:
+        ok4 = bool(torch.equal(got4, joints(0, G4)))
+        # and every shard's first frame recomputed alone (verify_gather's check)
+        ok4 = ok4 and all(bool(torch.equal(got4[s0], joints(s0, 1)[0])) for s0, _ in shards)
+    ident = rank_identity(None, rank, int(os.environ.get("LOCAL_RANK", rank)), True)
+    drec = dist_record(ident, world, dist.get_backend() if world > 1 else None)
     return dict(metric=METRIC, value=G * args.steps / elapsed, unit="frames/s", n_gpus=world, steps=args.steps,
                 warmup=args.warmup, ms_per_step=elapsed / args.steps * 1e3, higher_is_better=True, scaling="weak",
                 vs_baseline=None, dtype="f32", data="dry run: CPU/gloo protocol check, stand-in step (no HIP)",
-                dry_run=True, gather_verified=ok,
+                dry_run=True, gather_verified=ok, dist=drec,
                 config={"workload": "dry run of the config-2 sharding", "global_batch": G, "frames_per_gpu": B,
-                        "parallelism": f"dp{world}", "collective": "all_gather joints (gloo)" if world > 1 else None})
+                        "parallelism": f"dp{world}", "collective": "all_gather joints (gloo)" if world > 1 else None},
+                config4={"workload": "dry run of the config-4 sharding (128 frames split over the ranks)",
+                         "global_batch": G4, "value": G4 * args.steps / el4, "scaling": "strong",
+                         "shards": shards, "gather": {"gather_verified": ok4,
+                                                      "frames_recomputed": [s0 for s0, _ in shards]}})
 
 
 # ----------------------------------------------------------------------------- main
@@ -758,6 +849,9 @@ def main():
     ap.add_argument("--settle", type=float, default=1.0,
                     help="seconds of untimed steps before the warmup, per config (GPU clock ramp from idle)")
     ap.add_argument("--config", default="2", choices=["2", "3", "4"])
+    ap.add_argument("--precision", default="exact", choices=["exact", "fast"],
+                    help="the unprojection arithmetic of the headline and its secondary configs (DESIGN.md §4.1a); "
+                         "the other arithmetic is reported beside them")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-in-kernel-coords", action="store_true",
@@ -821,6 +915,19 @@ def main():
                          softargmax_ms=s["softargmax_ms"], roofline=roofline(s["cfg"], s, "3", device),
                          path_algorithmic_gbps=s["path_gbps"], path_frac=s["path_gbps"] / HBM_PEAK_GBPS,
                          telemetry=s["telemetry"])
+    other = other_res = None
+    if extras:
+        # the other unprojection arithmetic on configs 2 and 3, same protocol
+        alt = "fast" if args.precision == "exact" else "exact"
+        other_res = {"2": run_config("2", args, rank, world, device, clock, precision=alt),
+                     "3": run_config("3", args, rank, world, device, clock, precision=alt)}
+        other = {"precision": alt}
+        for cn, o in other_res.items():
+            other[f"config{cn}"] = dict(workload=o["cfg"]["label"], value=o["fps"], unit="frames/s",
+                                        ms_per_step=o["ms_per_step"], unproject_ms=o["unproject_ms"],
+                                        softargmax_ms=o["softargmax_ms"], roofline=roofline(o["cfg"], o, cn, device),
+                                        path_algorithmic_gbps=o["path_gbps"],
+                                        path_frac=o["path_gbps"] / HBM_PEAK_GBPS, telemetry=o["telemetry"])
     if not args.no_secondary and not args.no_in_kernel_coords:
         # the same workload with the coordinate volume formed inside both kernels from the
         # per-frame cuboids instead of read from HBM
@@ -862,6 +969,9 @@ def main():
             cfg4["parity"] = parity_check(r4)
         if cfg5 is not None and cfg5.get("parity_inputs") is not None:
             cfg5["parity"] = parity_check5(cfg5)
+        if other is not None:
+            for cn, o in other_res.items():
+                other[f"config{cn}"]["parity"] = parity_check(o)
     if cfg5 is not None:
         cfg5.pop("parity_inputs", None)
     gather = None
@@ -869,6 +979,19 @@ def main():
         gather = verify_gather(main_res)
         if cfg4 is not None:
             cfg4["gather"] = verify_gather(r4)
+        # rank 0's own shard of the timed outputs against the oracle (the checker, after
+        # every timed region), so that a multi-GPU line carries parity too
+        if not args.no_cpu_baseline:
+            parity = parity_check(main_res)
+            if cfg4 is not None:
+                cfg4["parity"] = parity_check(r4)
+    # the self-proving multi-rank record: backend, every rank's device, per-rank telemetry
+    drec = dist_record(rank_identity(device, rank, local, False), world,
+                       (dist.get_backend() if world > 1 else None))
+    tel_ranks = gather_objects(main_res["telemetry"], world) if world > 1 else None
+    tel4_ranks = gather_objects(r4["telemetry"], world) if (world > 1 and cfg4 is not None) else None
+    if cfg4 is not None:
+        cfg4["telemetry_per_rank"] = tel4_ranks
 
     if rank == 0:
         r, c = main_res, main_res["cfg"]
@@ -895,11 +1018,15 @@ def main():
             "path_algorithmic_gbps": r["path_gbps"],
             "path_frac": r["path_gbps"] / HBM_PEAK_GBPS,
             "telemetry": r["telemetry"],
+            "telemetry_per_rank": tel_ranks,
             "gpu": gpu_identity(device),
+            "dist": drec,
             "cpu_baseline": base,
             "parity": parity,
             "gather": gather,
+            "precision": args.precision,
             "secondary": secondary,
+            "other_precision": other,
             "config1": config1,
             "in_kernel_coords": in_kernel_coords,
             "config4": cfg4,

@@ -61,6 +61,13 @@ extern "C" {
 #define MVN_LAYOUT_NCDHW 0     /* (B, C, Vx, Vy, Vz): the reference's unproject output */
 #define MVN_LAYOUT_NDHWC 1     /* (B, Vx, Vy, Vz, C): channels-last (V2V front input)  */
 
+/* ---- unprojection arithmetic -------------------------------------------- */
+#define MVN_PRECISION_EXACT 0  /* the reference's f32 op order: sum / max / conf* bit-exact,
+                                  softmax <= 1e-5 (the default of every other entry point)  */
+#define MVN_PRECISION_FAST  1  /* the north_star contract's tolerance:
+                                  reciprocal projection, max-free view softmax, and for bf16
+                                  maps bf16 bilinear weights on v_dot2 pixel pairs          */
+
 /* ---- view aggregation (op.py:147-161) ---------------------------------- */
 #define MVN_AGG_SUM      0     /* 'sum'                                           */
 #define MVN_AGG_MAX      1     /* 'max'                                           */
@@ -142,6 +149,20 @@ int mvn_unproject_ex(const void* feat, int feat_dtype,
                      void* out, int out_dtype, int out_layout,
                      int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
                      int agg, int align_corners, void* stream);
+
+/*
+ * mvn_unproject / mvn_unproject_ex / mvn_unproject_cuboid with a selectable arithmetic
+ * (op.py:99-163).  Exactly one of coords (B, Vx, Vy, Vz, 3) and cuboids (B, 18; then
+ * Vx = Vy = Vz, N <= 8) is non-NULL.  precision = MVN_PRECISION_EXACT is bit-identical
+ * to those entry points; MVN_PRECISION_FAST computes the same function within the
+ * north_star tolerance (f32 maps: <= 1e-5 max-rel of the volume; bf16 maps: one bf16 ulp
+ * + 2^-8 max|ref|; validity masks unchanged), measured in DESIGN.md §4.1a.
+ */
+int mvn_unproject_precision(const void* feat, int feat_dtype,
+                            const float* proj, const float* coords, const float* cuboids, int transfer_cmu,
+                            const float* conf, void* out, int out_dtype, int out_layout,
+                            int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
+                            int agg, int align_corners, int precision, void* stream);
 
 /*
  * V2V front block, eval mode: Conv3d(32 -> 16, k = 7, pad = 3) + BatchNorm3d + ReLU

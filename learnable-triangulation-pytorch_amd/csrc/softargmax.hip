@@ -141,7 +141,12 @@ __device__ __forceinline__ float wave_sum63(float v) {
 
 // Max of a lane's values as a tree of three-operand maxima: 8 v_max3_f32 for 16 values.
 // (fmaxf on the raw loaded values would first canonicalise each input — one more v_max per
-// value in IEEE mode — so the instruction is written out.  NaNs are dropped as fmaxf does.)
+// value in IEEE mode — so the instruction is written out.)  NaN: v_max3_f32 / the DPP v_max
+// return the other operand for a quiet NaN, so the max of a chunk with some NaN voxels is
+// the max of the rest, and the max of an all-NaN chunk (or a signalling NaN) is NaN.  Either
+// way the NaN voxel's exponential is NaN, so the joint's sums, coordinates and normalised
+// volume are NaN — torch's softmax over a volume holding a NaN (op.py:89) is NaN everywhere
+// (tests/test_gpu_parity.py::test_softargmax_nan_volume_follows_torch).
 __device__ __forceinline__ float vmax3(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));

@@ -139,11 +139,11 @@ inline bool use_simple_kernel() { return unproject_force_simple(); }
 template <int AGG, typename TIn, typename TOut>
 int launch_agg(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
                const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
-               int align_corners, int out_cl, hipStream_t s) {
+               int align_corners, int out_cl, int fast, hipStream_t s) {
   const int nvox = Vx * Vy * Vz;
   if (N <= kMaxRegViews && !use_simple_kernel())
     return launch_tiled<AGG, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz,
-                                        align_corners, out_cl, s);
+                                        align_corners, out_cl, fast, s);
   if (cub) return MVN_ERR_SHAPE;     // in-kernel coordinates: the tiled kernel only (N <= 8)
   if (out_cl) return MVN_ERR_ARG;    // channels-last output: the tiled kernel only (N <= 8)
   dim3 grid((nvox + kUnprojBlock - 1) / kUnprojBlock, B);
@@ -161,16 +161,16 @@ int launch_agg(const void* feat, const float* P, const float* coords, const floa
 template <typename TIn, typename TOut>
 int launch_types(int agg, const void* feat, const float* P, const float* coords, const float* cub, int transfer,
                  const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
-                 int align_corners, int out_cl, hipStream_t s) {
+                 int align_corners, int out_cl, int fast, hipStream_t s) {
   switch (agg) {
     case MVN_AGG_SUM:
-      return launch_agg<MVN_AGG_SUM, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, out_cl, s);
+      return launch_agg<MVN_AGG_SUM, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, out_cl, fast, s);
     case MVN_AGG_MAX:
-      return launch_agg<MVN_AGG_MAX, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, out_cl, s);
+      return launch_agg<MVN_AGG_MAX, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, out_cl, fast, s);
     case MVN_AGG_SOFTMAX:
-      return launch_agg<MVN_AGG_SOFTMAX, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, out_cl, s);
+      return launch_agg<MVN_AGG_SOFTMAX, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, out_cl, fast, s);
     case MVN_AGG_CONF:
-      return launch_agg<MVN_AGG_CONF, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, out_cl, s);
+      return launch_agg<MVN_AGG_CONF, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz, align_corners, out_cl, fast, s);
   }
   return MVN_ERR_ARG;
 }
@@ -182,8 +182,11 @@ namespace mvn {
 namespace {
 int unproject_entry(const void* feat, int feat_dtype, const float* proj, const float* coords, const float* cub,
                     int transfer, const float* conf, void* out, int out_dtype, int out_layout, int B, int N, int C,
-                    int H, int W, int Vx, int Vy, int Vz, int agg, int align_corners, void* stream) {
+                    int H, int W, int Vx, int Vy, int Vz, int agg, int align_corners, int precision,
+                    void* stream) {
   if (!feat || !proj || !(coords || cub) || !out) return MVN_ERR_ARG;
+  if (precision != MVN_PRECISION_EXACT && precision != MVN_PRECISION_FAST) return MVN_ERR_ARG;
+  const int fast = precision == MVN_PRECISION_FAST;
   if (agg < MVN_AGG_SUM || agg > MVN_AGG_CONF) return MVN_ERR_ARG;
   if (agg == MVN_AGG_CONF && !conf) return MVN_ERR_ARG;
   if (align_corners != 0 && align_corners != 1) return MVN_ERR_ARG;
@@ -196,13 +199,13 @@ int unproject_entry(const void* feat, int feat_dtype, const float* proj, const f
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (feat_dtype == MVN_DTYPE_F32 && out_dtype == MVN_DTYPE_F32)
     return launch_types<float, float>(agg, feat, proj, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz,
-                                      align_corners, cl, s);
+                                      align_corners, cl, fast, s);
   if (feat_dtype == MVN_DTYPE_BF16 && out_dtype == MVN_DTYPE_BF16)
     return launch_types<uint16_t, uint16_t>(agg, feat, proj, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy,
-                                            Vz, align_corners, cl, s);
+                                            Vz, align_corners, cl, fast, s);
   if (feat_dtype == MVN_DTYPE_BF16 && out_dtype == MVN_DTYPE_F32)
     return launch_types<uint16_t, float>(agg, feat, proj, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz,
-                                         align_corners, cl, s);
+                                         align_corners, cl, fast, s);
   return MVN_ERR_DTYPE;
 }
 }  // namespace
@@ -277,7 +280,7 @@ extern "C" int mvn_unproject_ex(const void* feat, int feat_dtype, const float* p
                                 int H, int W, int Vx, int Vy, int Vz, int agg, int align_corners, void* stream) {
   if (!coords) return MVN_ERR_ARG;
   return mvn::unproject_entry(feat, feat_dtype, proj, coords, nullptr, 0, conf, out, out_dtype, out_layout, B, N, C,
-                              H, W, Vx, Vy, Vz, agg, align_corners, stream);
+                              H, W, Vx, Vy, Vz, agg, align_corners, MVN_PRECISION_EXACT, stream);
 }
 
 extern "C" int mvn_unproject_cuboid(const void* feat, int feat_dtype, const float* proj, const float* cuboids,
@@ -287,7 +290,17 @@ extern "C" int mvn_unproject_cuboid(const void* feat, int feat_dtype, const floa
   if (!cuboids) return MVN_ERR_ARG;
   if (N > mvn::kMaxRegViews) return MVN_ERR_SHAPE;
   return mvn::unproject_entry(feat, feat_dtype, proj, nullptr, cuboids, transfer_cmu, conf, out, out_dtype,
-                              out_layout, B, N, C, H, W, V, V, V, agg, align_corners, stream);
+                              out_layout, B, N, C, H, W, V, V, V, agg, align_corners, MVN_PRECISION_EXACT, stream);
+}
+
+extern "C" int mvn_unproject_precision(const void* feat, int feat_dtype, const float* proj, const float* coords,
+                                       const float* cuboids, int transfer_cmu, const float* conf, void* out,
+                                       int out_dtype, int out_layout, int B, int N, int C, int H, int W, int Vx,
+                                       int Vy, int Vz, int agg, int align_corners, int precision, void* stream) {
+  if ((coords == nullptr) == (cuboids == nullptr)) return MVN_ERR_ARG;     // exactly one coordinate source
+  if (cuboids && (N > mvn::kMaxRegViews || Vx != Vy || Vx != Vz)) return MVN_ERR_SHAPE;
+  return mvn::unproject_entry(feat, feat_dtype, proj, coords, cuboids, cuboids ? transfer_cmu : 0, conf, out,
+                              out_dtype, out_layout, B, N, C, H, W, Vx, Vy, Vz, agg, align_corners, precision, stream);
 }
 
 extern "C" int mvn_unproject(const void* feat, int feat_dtype, const float* proj, const float* coords,

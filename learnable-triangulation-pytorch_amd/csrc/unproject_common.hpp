@@ -289,7 +289,7 @@ template <int AGG, typename TIn, typename TOut>
 // Vx = Vy = Vz), see cuboid_coord in common.hpp.
 int launch_tiled(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
                  const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
-                 int align_corners, int out_cl, hipStream_t s);
+                 int align_corners, int out_cl, int fast, hipStream_t s);
 
 // ---- helpers of the chunk-staged kernel (unproject_x4.hip) ------------------------------
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -376,6 +376,52 @@ __device__ __forceinline__ f2 aggregate_pair(const f2 (&s)[NV], const f2 (&cf)[N
   }
 }
 
+// v_dot2_f32_bf16 with a zero accumulator in its VOP3P form: the builtin selects the VOP2
+// v_dot2c (accumulator = destination), which costs a v_mov of 0 per first row (16 per group
+// of the fast bf16 kernel).  Non-volatile: the scheduler places it like any VALU op.
+__device__ __forceinline__ float dot2_bf16_from0(uint32_t a, uint32_t w) {
+  float r;
+  asm("v_dot2_f32_bf16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(w));
+  return r;
+}
+// three-operand max / min (v_max3_f32 / v_min3_f32: quiet NaNs dropped, as fmaxf / fminf)
+__device__ __forceinline__ float vmax3f(float a, float b, float c) { return __builtin_fmaxf(a, __builtin_fmaxf(b, c)); }
+__device__ __forceinline__ float vmin3f(float a, float b, float c) { return __builtin_fminf(a, __builtin_fminf(b, c)); }
+
+// View softmax of a channel pair from log2-scaled samples t_v = s_v * log2(e) (the fast
+// unprojection, MVN_PRECISION_FAST): value = ln2 * sum_v t_v 2^t_v / sum_v 2^t_v, which is
+// sum_v s_v softmax_v(s).  MAXSUB = false skips the max pass (exact in real arithmetic; the
+// caller guards the denominator's range), true is the max-first form the guard falls back to.
+// den receives the denominators (of the form used).
+template <int NV, bool MAXSUB>
+__device__ __forceinline__ f2 softmax_pair_log2(const f2 (&t)[NV], f2& den) {
+  constexpr float kLn2 = 0.6931471805599453f;
+  f2 nm = f2{0.f, 0.f};
+  if constexpr (MAXSUB) {
+    f2 m = t[0];
+#pragma unroll
+    for (int v = 1; v < NV; ++v) {
+      m.x = fmaxf(m.x, t[v].x);
+      m.y = fmaxf(m.y, t[v].y);
+    }
+    nm = -m;
+  }
+  f2 e[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const f2 a = MAXSUB ? t[v] + nm : t[v];
+    e[v] = f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  }
+  den = e[0];
+  f2 num = t[0] * e[0];
+#pragma unroll
+  for (int v = 1; v < NV; ++v) {
+    den = den + e[v];
+    num = pk_fma(t[v], e[v], num);
+  }
+  return (num * f2{kLn2, kLn2}) * f2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+}
+
 // Cache policy of the four-view kernel's NCDHW output stores (2 = nt).  f32 planes stream
 // out non-temporally so that they do not evict the feature maps the next tiles re-read
 // (whole step at config 2: 261.5 -> 257.8 us); 2-byte bf16 stores must not (577 -> 1,664 us).
@@ -427,7 +473,7 @@ __device__ __forceinline__ Region pick_region(const Region (&rg)[NV], int u) {
 template <int AGG, typename TIn, typename TOut>
 int launch_x4(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
               const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
-              int align_corners, int out_cl, hipStream_t s);
+              int align_corners, int out_cl, int fast, hipStream_t s);
 
 }  // namespace unproj
 }  // namespace mvn

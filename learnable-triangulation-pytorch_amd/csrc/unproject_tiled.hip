@@ -468,11 +468,13 @@ __attribute__((amdgpu_waves_per_eu(TileShape<NV>::WAVES))) void unproject_tiled(
 template <int AGG, typename TIn, typename TOut>
 int launch_tiled(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
                  const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
-                 int align_corners, int out_cl, hipStream_t s) {
+                 int align_corners, int out_cl, int fast, hipStream_t s) {
   if (out_cl && C % 4 != 0) return MVN_ERR_SHAPE;
   if (!unproject_force_generic()) {
+    // (fast = MVN_PRECISION_FAST is a property of the chunk-staged kernel; where it does not
+    // apply the exact kernel below runs, which is inside the fast mode's tolerance)
     const int r = launch_x4<AGG, TIn, TOut>(feat, P, coords, cub, transfer, conf, out, B, N, C, H, W, Vx, Vy, Vz,
-                                            align_corners, out_cl, s);
+                                            align_corners, out_cl, fast, s);
     if (r != 1) return r;
   }
   // 32-bit buffer offsets: a frame's maps and volume must stay below 2 GiB
@@ -505,12 +507,12 @@ int launch_tiled(const void* feat, const float* P, const float* coords, const fl
 
 #define MVN_INSTANTIATE(AGG)                                                                                   \
   template int launch_tiled<AGG, float, float>(const void*, const float*, const float*, const float*, int, const float*, void*,    \
-                                               int, int, int, int, int, int, int, int, int, int, hipStream_t);       \
+                                               int, int, int, int, int, int, int, int, int, int, int, hipStream_t);  \
   template int launch_tiled<AGG, uint16_t, uint16_t>(const void*, const float*, const float*, const float*, int, const float*,     \
                                                      void*, int, int, int, int, int, int, int, int, int, int,   \
-                                                     hipStream_t);                                              \
+                                                     int, hipStream_t);                                              \
   template int launch_tiled<AGG, uint16_t, float>(const void*, const float*, const float*, const float*, int, const float*, void*, \
-                                                  int, int, int, int, int, int, int, int, int, int, hipStream_t);
+                                                  int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 MVN_INSTANTIATE(MVN_AGG_SUM)
 MVN_INSTANTIATE(MVN_AGG_MAX)
 MVN_INSTANTIATE(MVN_AGG_SOFTMAX)

@@ -113,7 +113,11 @@ template <int NV> struct RegionSet {
 // CL: channels-last output (config 5) — a compile-time layout, so that the NCDHW kernels'
 // output stores are straight-line code: the compiler's vmcnt for a staging commit then counts
 // exactly the stores issued after the loads it waits for.
-template <int AGG, typename TIn, typename TOut, int K, int CL>
+// FAST (MVN_PRECISION_FAST): the same function within the north_star
+// tolerance instead of the reference's rounding — reciprocal projection, the view softmax
+// without its max pass (log2-scaled samples, a range guard that falls back to the max-first
+// formula), and for bf16 maps pixel-pair slots sampled by v_dot2_f32_bf16 with bf16 weights.
+template <int AGG, typename TIn, typename TOut, int K, int CL, int FAST>
 __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_per_eu(X4Shape<K>::WAVES))) void unproject_x4(
     const TIn* __restrict__ feat, const float* __restrict__ P, const float* __restrict__ coords,
     const float* __restrict__ cub, int transfer, const float* __restrict__ conf, TOut* __restrict__ out, int B,
@@ -124,6 +128,16 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ;
   constexpr int kThreads = S::THREADS, kBuf = S::SLOTS, MC = S::MC, kWaves = kThreads / kWave;
   static_assert(TX * TY * TZ == kThreads, "one voxel per thread");
+  // PAIR: bf16 pixel-pair slots — dword k of the slot at pixel (x, y) holds channel k's
+  // (x, x+1) bf16 pair, so a voxel-view reads 2 slots (rows y0, y1) per 4 channels instead of
+  // 4, and each row is one v_dot2_f32_bf16 against the (west, east) bf16 weight pair.  A
+  // slot needs pixel x+4 of its chunk's right neighbour: chunks are dealt to a wave's lanes
+  // 63 at a time, lane 63 loading the next wave's first chunk only to hand it to lane 62
+  // (DPP wave_shl:1) and writing nothing.
+  constexpr bool PAIR = FAST != 0 && sizeof(TIn) == 2 && G == 4;
+  constexpr bool SMXF = FAST != 0 && AGG == MVN_AGG_SOFTMAX;   // samples carry a log2(e) factor
+  constexpr int kLanesW = PAIR ? kWave - 1 : kWave;               // chunks a wave owns per slot i
+  constexpr int kCap = MC * kWaves * kLanesW;                       // chunk capacity of one pass
   // per buffer: image slots [0, kTrash), 64 per-lane trash slots (the masked-off pixels of
   // a chunk are written there: no exec-mask branch per write), 2 zero slots
   constexpr int kZeroSlot = kBuf - 2, kTrash = kBuf - 2 - kWave;
@@ -196,9 +210,39 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   }
   int fx[NV], fy[NV];
   f2 wp[NV][2];                        // bilinear weights (nw, ne), (sw, se) per view
+  uint32_t wq[NV][2];                  // PAIR: the same as bf16 pairs (nw | ne << 16), (sw | se << 16)
   bool has[NV];
   // per-voxel geometry: footprint base pixel, bilinear weights, "samples the image" flag
   auto project_voxel = [&]() __attribute__((always_inline)) {
+    if constexpr (FAST != 0) {
+      // ix = u / H * W - 0.5 (align_corners=False) or u / H * (W - 1) (True), u = uh / wh:
+      // op.py:121-130 + grid_sample's unnormalisation folded into one reciprocal of the depth
+      // and one fma per axis.  The validity mask is the reference's (same wh, same compare).
+      const float fW = float(W), fH = float(H);
+      const float ax = (align_corners ? fW - 1.f : fW) * __builtin_amdgcn_rcpf(fH);
+      const float ay = (align_corners ? fH - 1.f : fH) * __builtin_amdgcn_rcpf(fW);
+      const float bo = align_corners ? 0.f : -0.5f;
+      // softmax: the weights carry log2(e), so each sample is s * log2(e) (aggregate below)
+      const float ks = SMXF ? kLog2e : 1.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const Homog hp = homog(Pb + v * 12, cx, cy, cz);
+        const float r = __builtin_amdgcn_rcpf(hp.wh == 0.f ? 1.f : hp.wh);
+        const float ix = __builtin_fmaf(hp.uh, ax * r, bo), iy = __builtin_fmaf(hp.vh, ay * r, bo);
+        const float fx0 = floorf(ix), fy0 = floorf(iy);
+        const bool h = act & !(hp.wh <= 0.f) & (fx0 >= -1.f) & (fx0 < fW) & (fy0 >= -1.f) & (fy0 < fH);
+        const float tx_ = ix - fx0, sx_ = 1.f - tx_, ty_ = (iy - fy0) * ks, sy_ = ks - ty_;
+        wp[v][0] = f2{h ? sy_ * sx_ : 0.f, h ? sy_ * tx_ : 0.f};
+        wp[v][1] = f2{h ? ty_ * sx_ : 0.f, h ? ty_ * tx_ : 0.f};
+        if constexpr (PAIR) {
+          wq[v][0] = pack_bf16x2(wp[v][0].x, wp[v][0].y);
+          wq[v][1] = pack_bf16x2(wp[v][1].x, wp[v][1].y);
+        }
+        fx[v] = h ? int(fx0) : 0; fy[v] = h ? int(fy0) : 0;
+        has[v] = h;
+      }
+      return;
+    }
     bool lane_fast = true;
 #pragma unroll
     for (int v = 0; v < NV; ++v) lane_fast &= div_core_safe(homog(Pb + v * 12, cx, cy, cz));
@@ -299,8 +343,8 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       else { x0 = 0; y0 = 0; }
       const Region r0 = make_region(x0, y0, bw, bh, 0, 0, 0);
       const int area = r0.pitch * bh, nch = r0.cend;
-      if (area > lim || nch > MC * kThreads) too_big = true;
-      if (snext + area > lim || cnext + nch > MC * kThreads) { ++pass; snext = 0; cnext = 0; }
+      if (area > lim || nch > kCap) too_big = true;
+      if (snext + area > lim || cnext + nch > kCap) { ++pass; snext = 0; cnext = 0; }
       rs.set(v, make_region(x0, y0, bw, bh, snext, cnext, pass));
       snext += area;
       cnext += nch;
@@ -308,7 +352,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     }
     npass = too_big ? -1 : pass + 1;
     total = chunks0;
-    MVN_DASSERT(too_big || (total <= MC * kThreads && snext <= lim));
+    MVN_DASSERT(too_big || (total <= kCap && snext <= lim));
   }
 
   if (npass < 0) {
@@ -343,6 +387,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   };
   // Chunk (k of a pass) -> global byte offset (kOob outside the image), first LDS slot and
   // the mask of its 4 pixels that lie in the view's box (empty past the pass's chunks).
+  const bool writer = !PAIR || lane != kWave - 1;      // PAIR: lane 63 only feeds lane 62
   auto chunk_fields = [&](const Region& r, int sel, int li, uint32_t& goff, int& s0, uint32_t& mask, bool live)
       __attribute__((always_inline)) {
     // li = row * cw + chunk column (rows fastest-varying outer)
@@ -352,10 +397,12 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     goff = in ? uint32_t((sel * C * HW + gy * W + gx) * int(E)) : kOob;
     s0 = r.sbase + py * r.pitch + (gx - r.x0);
     mask = 0;
+    // PAIR: the slot of pixel dx holds (dx, dx+1): the box's last column is never a base
+    const int xend = PAIR ? r.bw - 1 : r.bw;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int dx = gx + p - r.x0;
-      mask |= (live & (dx >= 0) & (dx < r.bw)) ? (1u << p) : 0u;
+      mask |= (live & writer & (dx >= 0) & (dx < xend)) ? (1u << p) : 0u;
     }
   };
   using Chunk = typename ChunkT<TIn>::type;
@@ -367,6 +414,24 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   // (no exec-mask branch per write), f32 maps on 4-channel slots branch (A/B at the bench
   // configs: each is the faster for its case; 8 views 694 -> 677 us, r16)
   auto write_group = [&](Slot* buf, const Chunk (&pre)[G], int s0, uint32_t mask) __attribute__((always_inline)) {
+    if constexpr (PAIR) {
+      // chunk dwords: lo = (px0, px1), hi = (px2, px3) of one channel; pixels 4, 5 are the
+      // right neighbour lane's lo.  Slot p, dword k: channel k's (px p, px p+1).
+      uint32_t nb[G];
+#pragma unroll
+      for (int k = 0; k < G; ++k) nb[k] = uint32_t(__builtin_amdgcn_mov_dpp(int(pre[k].x), 0x130, 0xf, 0xf, true));
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        uint32_t d[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+          d[k] = p == 0 ? pre[k].x : p == 1 ? __builtin_amdgcn_alignbit(pre[k].y, pre[k].x, 16)
+               : p == 2 ? pre[k].y : __builtin_amdgcn_alignbit(nb[k], pre[k].y, 16);
+        MVN_DASSERT(!(mask & (1u << p)) || (s0 + p >= 0 && s0 + p < kTrash));
+        buf[(mask & (1u << p)) ? s0 + p : kTrash + lane] = make_uint4(d[0], d[1], d[2], d[3]);
+      }
+      return;
+    }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       Slot q;
@@ -402,6 +467,24 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (!all && rs.get(v).pass != pass) continue;
+      if constexpr (PAIR) {
+        // two slots per view (rows y0, y1), one v_dot2_f32_bf16 per row and channel
+        const Slot a = tap(buf + anw[v]);
+        const Slot cq = tap(buf + asw[v]);
+        const bf16x2_t w1 = __builtin_bit_cast(bf16x2_t, wq[v][1]);
+        const uint32_t an[4] = {a.x, a.y, a.z, a.w}, as[4] = {cq.x, cq.y, cq.z, cq.w};
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+          float o[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            o[h] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, as[2 * q + h]), w1,
+                                                   dot2_bf16_from0(an[2 * q + h], wq[v][0]), false);
+          sv[q][v] = f2{o[0], o[1]};
+        }
+        if (v & 1) __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
       const Slot a = tap(buf + anw[v]);
       const Slot bq = tap(buf + anw[v] + kSlotB);
       const Slot cq = tap(buf + asw[v]);
@@ -414,11 +497,60 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       if (v & 1) __builtin_amdgcn_sched_barrier(0);   // at most two views' taps in flight
     }
   };
+  // SMXF: range of the max-free softmax's denominators over every channel of this voxel.
+  // Outside [2^-100, 2^120] (|s| beyond ~70: overflow, or underflow in every view) the wave
+  // recomputes its voxels with the exact gather path after the channel loop (rare; NaNs do
+  // not trip it — a NaN sample gives a NaN value in either form, as in the reference).
+  constexpr bool kDeferredGuard = NV == 4 && (sizeof(TIn) == 2 || CL == 0);   // (f32 channels-last: spills)
+  float dmx = 0.f, dmn = INFINITY;
+  auto range_fallback = [&]() __attribute__((always_inline)) {
+    if constexpr (SMXF && kDeferredGuard) {
+      if (__builtin_amdgcn_ballot_w64(!(dmx <= 0x1p120f) || !(dmn >= 0x1p-100f))) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the fast values' stores land first
+        if (act)
+          gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + (out_cl ? size_t(vox) * C : vox),
+                                       out_cl ? 1 : nvox, NV, C, H, W, cx, cy, cz, align_corners);
+      }
+    }
+  };
   constexpr int NG = 4;                    // bf16 channels-last: groups per run of 16-byte stores
   uint2 cl_buf[NG - 1];
 #pragma unroll
   for (int k = 0; k < NG - 1; ++k) cl_buf[k] = make_uint2(0u, 0u);
   auto aggregate = [&](int c0, const f2 (&sv)[NP][NV], float (&r)[G]) __attribute__((always_inline)) {
+    if constexpr (SMXF) {
+      // max-free softmax of the log2-scaled samples; the denominators' range is tracked over
+      // all groups and checked once per voxel at the end (range_fallback).  8 views: at the
+      // register limit of 3 waves per SIMD the loop-carried range spills, so the group checks
+      // its own range and redoes itself max-first.
+      float gmx = 0.f, gmn = INFINITY;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        f2 den;
+        const f2 o = softmax_pair_log2<NV, false>(sv[q], den);
+        if constexpr (kDeferredGuard) {
+          dmx = vmax3f(dmx, den.x, den.y);
+          dmn = vmin3f(dmn, den.x, den.y);
+        } else {
+          gmx = vmax3f(gmx, den.x, den.y);
+          gmn = vmin3f(gmn, den.x, den.y);
+        }
+        r[2 * q] = o.x;
+        r[2 * q + 1] = o.y;
+      }
+      if constexpr (!kDeferredGuard) {
+        if (__builtin_amdgcn_ballot_w64(!(gmx <= 0x1p120f) || !(gmn >= 0x1p-100f))) {
+#pragma unroll
+          for (int q = 0; q < NP; ++q) {
+            f2 den;
+            const f2 o = softmax_pair_log2<NV, true>(sv[q], den);
+            r[2 * q] = o.x;
+            r[2 * q + 1] = o.y;
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       f2 cf[NV];
@@ -493,7 +625,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     int s0[MC];
 #pragma unroll
     for (int i = 0; i < MC; ++i) {
-      const int k = t + kThreads * i;
+      const int k = i * kWaves * kLanesW + wid * kLanesW + lane;     // = t + kThreads * i unless PAIR
       int sel = 0;
 #pragma unroll
       for (int u = 1; u < NV; ++u)
@@ -501,17 +633,17 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       const Region r = rs.pick(sel);
       chunk_fields(r, sel, k - r.cbase, goff[i], s0[i], mask[i], k < total);
     }
-    const int wfirst = __builtin_amdgcn_readfirstlane(wid * kWave);
+    const int wfirst = __builtin_amdgcn_readfirstlane(wid * kLanesW);
     Chunk pre[MC][G];
     auto issue = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < MC; ++i)
-        if (wfirst + kThreads * i < total) load_group(pre[i], goff[i], c0);
+        if (wfirst + kWaves * kLanesW * i < total) load_group(pre[i], goff[i], c0);
     };
     auto commit = [&](Slot* buf) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < MC; ++i)
-        if (wfirst + kThreads * i < total) write_group(buf, pre[i], s0[i], mask[i]);
+        if (wfirst + kWaves * kLanesW * i < total) write_group(buf, pre[i], s0[i], mask[i]);
     };
     issue(0);
     tap_slots();
@@ -538,6 +670,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
       store_out(c0 + G, r);
       __syncthreads();
     }
+    range_fallback();
     return;
   }
 
@@ -551,7 +684,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
         const Region rv = rs.get(v);
         if (rv.pass != pass) continue;
         const int nch = rv.cend - rv.cbase;
-        for (int li = t; li < nch; li += kThreads) {
+        for (int li = wid * kLanesW + lane; li < nch; li += kWaves * kLanesW) {
           uint32_t goff, mask;
           int s0;
           chunk_fields(rv, v, li, goff, s0, mask, true);
@@ -568,6 +701,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     aggregate(c0, sv, r);
     store_out(c0, r);
   }
+  range_fallback();
 }
 
 }  // namespace
@@ -577,7 +711,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
 template <int AGG, typename TIn, typename TOut>
 int launch_x4(const void* feat, const float* P, const float* coords, const float* cub, int transfer,
               const float* conf, void* out, int B, int N, int C, int H, int W, int Vx, int Vy, int Vz,
-              int align_corners, int out_cl, hipStream_t s) {
+              int align_corners, int out_cl, int fast, hipStream_t s) {
   if (H > 32000 || W > 32000 || W % 4 != 0) return 1;
   // 4 views: tile per input dtype (A/B at the bench configs), f32 4x8x16,
   // bf16 4x8x8; 8 views: 2-channel slots, NCDHW output only
@@ -594,9 +728,14 @@ int launch_x4(const void* feat, const float* P, const float* coords, const float
     const long long nb = (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) *
                          ((Vz + S::TZ - 1) / S::TZ);
     if (nb > INT_MAX) return MVN_ERR_SHAPE;
-    unproject_x4<AGG, TIn, TOut, K, CL><<<int(nb), S::THREADS, 0, s>>>(
-        static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, C, H, W, Vx, Vy,
-        Vz, align_corners, budget);
+    if (fast)
+      unproject_x4<AGG, TIn, TOut, K, CL, 1><<<int(nb), S::THREADS, 0, s>>>(
+          static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, C, H, W, Vx, Vy,
+          Vz, align_corners, budget);
+    else
+      unproject_x4<AGG, TIn, TOut, K, CL, 0><<<int(nb), S::THREADS, 0, s>>>(
+          static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, C, H, W, Vx, Vy,
+          Vz, align_corners, budget);
     return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
   };
   using NC = std::integral_constant<int, 0>;
@@ -610,9 +749,9 @@ int launch_x4(const void* feat, const float* P, const float* coords, const float
 int x4_blocks_per_cu(int bf16) {
   int n = 0;
   const hipError_t e =
-      bf16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, unproject_x4<MVN_AGG_SOFTMAX, uint16_t, uint16_t, 2, 0>,
+      bf16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, unproject_x4<MVN_AGG_SOFTMAX, uint16_t, uint16_t, 2, 0, 0>,
                                                           X4Shape<2>::THREADS, 0)
-           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, unproject_x4<MVN_AGG_SOFTMAX, float, float, 0, 0>,
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, unproject_x4<MVN_AGG_SOFTMAX, float, float, 0, 0, 0>,
                                                           X4Shape<0>::THREADS, 0);
   return e == hipSuccess ? n : MVN_ERR_LAUNCH;
 }
@@ -620,13 +759,13 @@ int x4_blocks_per_cu(int bf16) {
 #define MVN_INSTANTIATE(AGG)                                                                                   \
   template int launch_x4<AGG, float, float>(const void*, const float*, const float*, const float*, int,        \
                                             const float*, void*, int, int, int, int, int, int, int, int, int,  \
-                                            int, hipStream_t);                                                 \
+                                            int, int, hipStream_t);                                            \
   template int launch_x4<AGG, uint16_t, uint16_t>(const void*, const float*, const float*, const float*, int,  \
                                                   const float*, void*, int, int, int, int, int, int, int, int, \
-                                                  int, int, hipStream_t);                                      \
+                                                  int, int, int, hipStream_t);                                      \
   template int launch_x4<AGG, uint16_t, float>(const void*, const float*, const float*, const float*, int,     \
                                                const float*, void*, int, int, int, int, int, int, int, int,    \
-                                               int, int, hipStream_t);
+                                               int, int, int, hipStream_t);
 MVN_INSTANTIATE(MVN_AGG_SUM)
 MVN_INSTANTIATE(MVN_AGG_MAX)
 MVN_INSTANTIATE(MVN_AGG_SOFTMAX)

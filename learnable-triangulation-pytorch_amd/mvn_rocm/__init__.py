@@ -16,9 +16,10 @@ from __future__ import annotations
 from . import _lib
 from . import op, multiview
 
-__all__ = ["op", "multiview", "install", "library_path"]
+__all__ = ["op", "multiview", "install", "library_path", "set_unproject_precision"]
 
 library_path = _lib.LIB_PATH
+set_unproject_precision = op.set_unproject_precision
 
 
 def install(mvn_op=None, mvn_multiview=None):

@@ -20,6 +20,7 @@ MVN_DTYPE_F32 = 0
 MVN_DTYPE_BF16 = 1
 MVN_AGG_SUM, MVN_AGG_MAX, MVN_AGG_SOFTMAX, MVN_AGG_CONF = 0, 1, 2, 3
 MVN_LAYOUT_NCDHW, MVN_LAYOUT_NDHWC = 0, 1
+MVN_PRECISION_EXACT, MVN_PRECISION_FAST = 0, 1
 
 _c_int, _c_void_p, _c_float, _c_i64, _c_size_t = (
     ctypes.c_int, ctypes.c_void_p, ctypes.c_float, ctypes.c_int64, ctypes.c_size_t)
@@ -46,6 +47,8 @@ SIGNATURES = {
     "mvn_nearest_voxel": (_c_int, [_c_void_p] * 3 + [_c_int] * 5 + [_c_void_p]),
     "mvn_unproject_ex": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int]
                          + [_c_int] * 8 + [_c_int, _c_int, _c_void_p]),
+    "mvn_unproject_precision": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p,
+                                         _c_void_p, _c_int, _c_int] + [_c_int] * 8 + [_c_int, _c_int, _c_int, _c_void_p]),
     "mvn_unproject_v2v_front_workspace_bytes": (_c_size_t, [_c_int, _c_int]),
     "mvn_unproject_v2v_front": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_size_t,

@@ -86,24 +86,32 @@ def call(op, *args):
 # --------------------------------------------------------------------------- unproject
 @_op("unproject")
 def unproject(feat: Tensor, proj: Tensor, coords: Tensor, conf: Optional[Tensor], agg: int,
-              align_corners: bool, out_dtype: int) -> Tensor:
+              align_corners: bool, out_dtype: int, precision: int = 0) -> Tensor:
     """feat (B,N,C,H,W) f32|bf16, proj (B,N,3,4) f32, coords (B,Vx,Vy,Vz,3) f32,
-    conf (B,N,C) f32 or None -> (B,C,Vx,Vy,Vz) of dtype code `out_dtype`."""
+    conf (B,N,C) f32 or None -> (B,C,Vx,Vy,Vz) of dtype code `out_dtype`; `precision`
+    MVN_PRECISION_EXACT (the reference's rounding) or MVN_PRECISION_FAST."""
     _require_gpu(feat, proj, coords, conf)
     B, N, C, H, W = feat.shape
     Vx, Vy, Vz = coords.shape[1:4]
     out = torch.empty((B, C, Vx, Vy, Vz), dtype=_CODE_DTYPE[out_dtype], device=feat.device)
     if out.numel() == 0:                  # empty batch: the reference returns the empty volume
         return out
-    code = _lib.load().mvn_unproject(
-        feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), coords.data_ptr(), _ptr(conf),
-        out.data_ptr(), out_dtype, B, N, C, H, W, Vx, Vy, Vz, agg, int(align_corners), _stream(feat))
+    lib = _lib.load()
+    if precision == _lib.MVN_PRECISION_EXACT:
+        code = lib.mvn_unproject(
+            feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), coords.data_ptr(), _ptr(conf),
+            out.data_ptr(), out_dtype, B, N, C, H, W, Vx, Vy, Vz, agg, int(align_corners), _stream(feat))
+    else:
+        code = lib.mvn_unproject_precision(
+            feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), coords.data_ptr(), None, 0, _ptr(conf),
+            out.data_ptr(), out_dtype, _lib.MVN_LAYOUT_NCDHW, B, N, C, H, W, Vx, Vy, Vz, agg, int(align_corners),
+            int(precision), _stream(feat))
     _lib.check(code, "mvn_unproject")
     return out
 
 
 @unproject.register_fake
-def _(feat, proj, coords, conf, agg, align_corners, out_dtype):
+def _(feat, proj, coords, conf, agg, align_corners, out_dtype, precision=0):
     B, N, C, H, W = feat.shape
     return feat.new_empty((B, C, *coords.shape[1:4]), dtype=_CODE_DTYPE[out_dtype])
 
@@ -144,7 +152,8 @@ def _(vol, coords, softmax, multiplier, return_volume, out_dtype):
 # --------------------------------------------------------------------------- in-kernel coordinates
 @_op("unproject_cuboid")
 def unproject_cuboid(feat: Tensor, proj: Tensor, cuboids: Tensor, volume_size: int, transfer: bool,
-                     conf: Optional[Tensor], agg: int, align_corners: bool, out_dtype: int) -> Tensor:
+                     conf: Optional[Tensor], agg: int, align_corners: bool, out_dtype: int,
+                     precision: int = 0) -> Tensor:
     """unproject with coordinates formed in-kernel from cuboids (B, 18) f32 (V^3 grid)."""
     _require_gpu(feat, proj, cuboids, conf)
     B, N, C, H, W = feat.shape
@@ -152,15 +161,16 @@ def unproject_cuboid(feat: Tensor, proj: Tensor, cuboids: Tensor, volume_size: i
     out = torch.empty((B, C, V, V, V), dtype=_CODE_DTYPE[out_dtype], device=feat.device)
     if out.numel() == 0:
         return out
-    code = _lib.load().mvn_unproject_cuboid(
-        feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), cuboids.data_ptr(), int(transfer), _ptr(conf),
-        out.data_ptr(), out_dtype, _lib.MVN_LAYOUT_NCDHW, B, N, C, H, W, V, agg, int(align_corners), _stream(feat))
+    code = _lib.load().mvn_unproject_precision(
+        feat.data_ptr(), _DTYPE_CODE[feat.dtype], proj.data_ptr(), None, cuboids.data_ptr(), int(transfer), _ptr(conf),
+        out.data_ptr(), out_dtype, _lib.MVN_LAYOUT_NCDHW, B, N, C, H, W, V, V, V, agg, int(align_corners),
+        int(precision), _stream(feat))
     _lib.check(code, "mvn_unproject_cuboid")
     return out
 
 
 @unproject_cuboid.register_fake
-def _(feat, proj, cuboids, volume_size, transfer, conf, agg, align_corners, out_dtype):
+def _(feat, proj, cuboids, volume_size, transfer, conf, agg, align_corners, out_dtype, precision=0):
     B, N, C = feat.shape[:3]
     V = int(volume_size)
     return feat.new_empty((B, C, V, V, V), dtype=_CODE_DTYPE[out_dtype])

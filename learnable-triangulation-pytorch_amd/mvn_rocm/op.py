@@ -12,6 +12,27 @@ from . import _lib
 from . import _ops
 
 _AGG = {"sum": _lib.MVN_AGG_SUM, "max": _lib.MVN_AGG_MAX, "softmax": _lib.MVN_AGG_SOFTMAX}
+_PRECISION = {"exact": _lib.MVN_PRECISION_EXACT, "fast": _lib.MVN_PRECISION_FAST}
+_default_precision = "exact"
+
+
+def set_unproject_precision(precision: str) -> str:
+    """Process-wide default arithmetic of ``unproject_heatmaps`` calls that pass no
+    ``precision=`` (as ``torch.backends`` flags do for matmul): ``'exact'`` (the default: the
+    reference's f32 rounding, 'sum' / 'max' / 'conf*' bit-exact) or ``'fast'`` (the north_star
+    tolerance) — the switch for a model rebound by ``install()``.  Returns the
+    previous setting."""
+    global _default_precision
+    precision_code(precision)
+    prev, _default_precision = _default_precision, precision
+    return prev
+
+
+def precision_code(precision) -> int:
+    p = _default_precision if precision is None else precision
+    if p not in _PRECISION:
+        raise ValueError(f"Unknown unprojection precision: {p!r} (expected 'exact' or 'fast')")
+    return _PRECISION[p]
 
 
 def aggregation_code(method: str) -> int:
@@ -65,7 +86,7 @@ def unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, method, cub
 
 
 def unproject_heatmaps(heatmaps, proj_matricies, coord_volumes, volume_aggregation_method='sum',
-                       vol_confidences=None, *, align_corners=False, out_dtype=None):
+                       vol_confidences=None, *, align_corners=False, out_dtype=None, precision=None):
     """Lift N views of C-channel maps into a (B, C, Vx, Vy, Vz) volume.
 
     Reference: ``mvn/utils/op.py:99-163``.
@@ -73,9 +94,12 @@ def unproject_heatmaps(heatmaps, proj_matricies, coord_volumes, volume_aggregati
       volume_aggregation_method in {'sum', 'max', 'softmax', 'conf*'}, vol_confidences (B, N, C).
     ``align_corners`` selects grid_sample semantics (False = torch>=1.3, the importable
     oracle; True = the torch 1.0.1 the reference pins).  ``out_dtype`` defaults to the
-    heatmap dtype (float32 for float32 input, as in the reference).
+    heatmap dtype (float32 for float32 input, as in the reference).  ``precision`` —
+    ``'exact'`` or ``'fast'``, default ``set_unproject_precision``'s — selects the arithmetic
+    (DESIGN.md §4.1a); the backward is the exact function's in both.
     """
     agg = aggregation_code(volume_aggregation_method)
+    prec = precision_code(precision)
     cub = coord_volumes if _is_cuboids(coord_volumes) else None
     feat, proj, conf = unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, volume_aggregation_method, cub)
     od = _dtype_code(out_dtype if out_dtype is not None else feat.dtype)
@@ -84,7 +108,7 @@ def unproject_heatmaps(heatmaps, proj_matricies, coord_volumes, volume_aggregati
             # in-kernel coordinates need the tiled kernel (N <= 8): materialise the volume
             coord_volumes, cub = cub.coord_volumes(), None
         else:
-            args = (feat, proj, cub.params, cub.volume_size, cub.transfer, conf, agg, bool(align_corners), od)
+            args = (feat, proj, cub.params, cub.volume_size, cub.transfer, conf, agg, bool(align_corners), od, prec)
             if _needs_grad(feat, conf):
                 return UnprojectCuboidFunction.apply(*args)
             return _ops.call(_ops.unproject_cuboid, *args)
@@ -92,8 +116,8 @@ def unproject_heatmaps(heatmaps, proj_matricies, coord_volumes, volume_aggregati
     if coords.dim() != 5 or coords.shape[0] != feat.shape[0] or coords.shape[4] != 3:
         raise RuntimeError(f"coord_volumes must be (B, Vx, Vy, Vz, 3), got {tuple(coords.shape)}")
     if _needs_grad(feat, conf):
-        return UnprojectFunction.apply(feat, proj, coords, conf, agg, bool(align_corners), od)
-    return _ops.call(_ops.unproject, feat, proj, coords, conf, agg, bool(align_corners), od)
+        return UnprojectFunction.apply(feat, proj, coords, conf, agg, bool(align_corners), od, prec)
+    return _ops.call(_ops.unproject, feat, proj, coords, conf, agg, bool(align_corners), od, prec)
 
 
 def integrate_tensor_3d_with_coordinates(volumes, coord_volumes, softmax=True, *, multiplier=1.0,
@@ -157,8 +181,8 @@ class UnprojectFunction(torch.autograd.Function):
     features and, for 'conf*', the confidences)."""
 
     @staticmethod
-    def forward(ctx, feat, proj, coords, conf, agg, align_corners, out_dtype):
-        out = _ops.call(_ops.unproject, feat, proj, coords, conf, agg, align_corners, out_dtype)
+    def forward(ctx, feat, proj, coords, conf, agg, align_corners, out_dtype, precision=_lib.MVN_PRECISION_EXACT):
+        out = _ops.call(_ops.unproject, feat, proj, coords, conf, agg, align_corners, out_dtype, precision)
         ctx.save_for_backward(feat, proj, coords, conf)
         ctx.cfg = (agg, align_corners)
         return out
@@ -166,7 +190,7 @@ class UnprojectFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out):
         from . import _backward
-        return _backward.unproject_backward(ctx, grad_out)
+        return _backward.unproject_backward(ctx, grad_out) + (None,)
 
 
 class SoftArgmaxFunction(torch.autograd.Function):
@@ -191,8 +215,10 @@ class UnprojectCuboidFunction(torch.autograd.Function):
     (one small kernel) and runs the same backward kernel."""
 
     @staticmethod
-    def forward(ctx, feat, proj, cub, V, transfer, conf, agg, align_corners, out_dtype):
-        out = _ops.call(_ops.unproject_cuboid, feat, proj, cub, V, transfer, conf, agg, align_corners, out_dtype)
+    def forward(ctx, feat, proj, cub, V, transfer, conf, agg, align_corners, out_dtype,
+                precision=_lib.MVN_PRECISION_EXACT):
+        out = _ops.call(_ops.unproject_cuboid, feat, proj, cub, V, transfer, conf, agg, align_corners, out_dtype,
+                        precision)
         ctx.save_for_backward(feat, proj, cub, conf)
         ctx.cfg = (V, transfer, agg, align_corners)
         return out
@@ -205,11 +231,11 @@ class UnprojectCuboidFunction(torch.autograd.Function):
         V, transfer, agg, align_corners = ctx.cfg
         want_conf = conf is not None and ctx.needs_input_grad[5]
         if not (ctx.needs_input_grad[0] or want_conf):
-            return (None,) * 9
+            return (None,) * 10
         coords = Cuboids(cub, V, transfer).coord_volumes()
         gfeat, gconf = _ops.call(_backward.unproject_bwd, feat, proj, coords, conf, grad_out, agg, align_corners, want_conf)
         return (gfeat if ctx.needs_input_grad[0] else None, None, None, None, None,
-                gconf if want_conf else None, None, None, None)
+                gconf if want_conf else None, None, None, None, None)
 
 
 class SoftArgmaxCuboidFunction(torch.autograd.Function):

@@ -61,13 +61,25 @@ def v2v_front(vol_cl, packed, scale, shift, out_dtype=torch.float32):
     return out
 
 
+def _inference_only(what, *tensors):
+    """The channels-last unprojection and the fused V2V front block have no backward: refuse
+    a call autograd would record (ADVICE r5 — a 'conf*' training caller would otherwise get a
+    volume without grad and lose the confidence gradient silently).  Training goes through
+    ``op.unproject_heatmaps`` (differentiable in the features and the confidences)."""
+    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors):
+        raise RuntimeError(f"{what} is inference-only (no backward): call it under torch.no_grad(), or use "
+                           "mvn_rocm.op.unproject_heatmaps, which is differentiable in the features and the "
+                           "confidences")
+
+
 def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggregation_method="softmax",
                             out_dtype=torch.bfloat16, align_corners=False, vol_confidences=None):
     """unproject_heatmaps (op.py:99-163) written channels-last: (B, Vx, Vy, Vz, C).
     ``coord_volumes`` may be a ``volumetric.Cuboids`` (coordinates formed in-kernel);
     ``vol_confidences`` (B, N, C) is read for 'conf*' aggregation (op.py:147-148), as
-    ``unproject_heatmaps``'s."""
+    ``unproject_heatmaps``'s.  Inference-only: no backward (training: ``op.unproject_heatmaps``)."""
     from .volumetric import Cuboids
+    _inference_only("unproject_channels_last", heatmaps, vol_confidences)
     agg = aggregation_code(volume_aggregation_method)
     cub = coord_volumes if isinstance(coord_volumes, Cuboids) else None
     feat, proj, conf = unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, volume_aggregation_method, cub)
@@ -145,8 +157,10 @@ def unproject_v2v_front(heatmaps, proj_matricies, coord_volumes, packed, scale, 
     groups through a workspace of one group's intermediate (default: 8 frames at V = 64,
     within half of the MALL).  ``coord_volumes`` may be a ``volumetric.Cuboids``.  Equal to
     ``v2v_front(unproject_channels_last(...))`` bit for bit.  'conf*' aggregation reads
-    ``vol_confidences`` (B, N, C), as the volumetric model does (triangulation.py:349)."""
+    ``vol_confidences`` (B, N, C), as the volumetric model does (triangulation.py:349).
+    Inference-only: no backward (the eval-mode BatchNorm fold is inference by construction)."""
     from .volumetric import Cuboids
+    _inference_only("unproject_v2v_front", heatmaps, vol_confidences)
     agg = aggregation_code(volume_aggregation_method)
     cub = coord_volumes if isinstance(coord_volumes, Cuboids) else None
     feat, proj, conf = unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, volume_aggregation_method, cub)

@@ -31,6 +31,27 @@ def test_bench_spawns_the_ranks(gpus):
     assert line["steps"] == 3 and line["warmup"] == 1 and line["value"] > 0
 
 
+@pytest.mark.parametrize("gpus", (5, 8))
+def test_bench_dry_run_config4_shards_and_dist_record(gpus):
+    """the multi-rank line proves itself — backend, every rank's identity,
+    one entry per rank — and config 4's 128 frames split over a ragged (5) or even (8) world
+    are gathered in frame order, every shard's first frame recomputed on rank 0."""
+    line = _bench("--gpus", str(gpus), "--dry-run", "--steps", "2", "--warmup", "1", timeout=420)
+    d = line["dist"]
+    assert d["backend"] == "gloo" and d["world"] == gpus
+    assert [r["rank"] for r in d["ranks"]] == list(range(gpus))
+    assert [r["local_rank"] for r in d["ranks"]] == list(range(gpus))
+    assert len({r["pid"] for r in d["ranks"]}) == gpus
+    c4 = line["config4"]
+    assert c4["global_batch"] == 128 and c4["scaling"] == "strong"
+    counts = [c for _, c in c4["shards"]]
+    assert sum(counts) == 128 and max(counts) - min(counts) <= 1
+    assert [s for s, _ in c4["shards"]] == [sum(counts[:r]) for r in range(gpus)]
+    assert c4["gather"]["gather_verified"] is True
+    assert c4["gather"]["frames_recomputed"] == [s for s, _ in c4["shards"]]
+    assert line["gather_verified"] is True
+
+
 def test_bench_a_failing_rank_ends_the_job():
     """Rank 1 dies before the first barrier (--dry-run-fail-rank): the launcher sees it while
     rank 0 is still blocked in the barrier, terminates rank 0 and exits non-zero — instead of

@@ -87,6 +87,49 @@ def test_unproject_argument_validation(lib):
     assert _unproject(lib, fdt=0, odt=1) == -3               # f32 features -> bf16 volume unsupported
 
 
+def test_unproject_precision_argument_validation(lib):
+    """mvn_unproject_precision: exactly one coordinate source, a known precision, cuboids only
+    for cubic volumes of <= 8 views — all checked before any HIP call."""
+    def call(**kw):
+        a = dict(coords=1, cub=None, N=4, Vz=64, prec=1)
+        a.update(kw)
+        return lib.mvn_unproject_precision(1, 0, 1, a["coords"], a["cub"], 0, None, 1, 0, 0, 1, a["N"], 32, 96, 96,
+                                           64, 64, a["Vz"], 2, 0, a["prec"], None)
+    assert call(coords=None) == -1
+    assert call(coords=1, cub=1) == -1
+    assert call(prec=2) == -1
+    assert call(prec=-1) == -1
+    assert call(coords=None, cub=1, Vz=32) == -2
+    assert call(coords=None, cub=1, N=9) == -2
+    from mvn_rocm import op
+    with pytest.raises(ValueError, match="Unknown unprojection precision"):
+        op.precision_code("fp8")
+    with pytest.raises(ValueError):
+        op.set_unproject_precision("approximate")
+    assert op.precision_code(None) == op.precision_code("exact") == 0 and op.precision_code("fast") == 1
+    prev = op.set_unproject_precision("fast")
+    try:
+        assert op.precision_code(None) == 1
+    finally:
+        op.set_unproject_precision(prev)
+
+
+def test_channels_last_paths_refuse_autograd():
+    """ADVICE r5: the channels-last unprojection and the one-call V2V pipeline have no backward;
+    with grad mode on and a feature or confidence tensor that requires grad they raise instead
+    of returning a volume whose confidence gradient is silently lost."""
+    from mvn_rocm import v2v
+    feat = torch.zeros(1, 4, 32, 8, 8)
+    conf = torch.ones(1, 4, 32, requires_grad=True)
+    P, coords = torch.zeros(1, 4, 3, 4), torch.zeros(1, 4, 4, 4, 3)
+    with pytest.raises(RuntimeError, match="inference-only"):
+        v2v.unproject_channels_last(feat, P, coords, "conf", vol_confidences=conf)
+    with pytest.raises(RuntimeError, match="inference-only"):
+        v2v.unproject_v2v_front(feat.requires_grad_(), P, coords, None, None, None, "softmax")
+    with torch.no_grad(), pytest.raises(RuntimeError, match="no CPU fallback"):
+        v2v.unproject_channels_last(feat, P, coords, "conf", vol_confidences=conf)
+
+
 def test_softargmax_argument_validation(lib):
     ws = lib.mvn_softargmax3d_workspace_bytes(32, 17, 64, 64, 64)
     assert ws == 32 * 17 * (256 * 5 + 2) * 4          # 1024-voxel partial chunks

@@ -275,6 +275,10 @@ def test_unproject_backward_direct_path_partial_tiles_nonfinite(device, mode, me
     conf = torch.from_numpy(np.random.default_rng(8).uniform(0.2, 1.0, (2, 4, 4)).astype(np.float32)) \
         if method == "conf" else None
     gout = torch.randn((2, 4, 13, 13, 13), generator=torch.Generator().manual_seed(9))
+    # the path under test: every 4x8x8 tile's footprints (pitch x rows, summed over the views)
+    # exceed the backward's 1,022 LDS slots (unproject_bwd.hip kZero), so no tile stages
+    from test_gpu_parity import tile_footprints
+    assert (tile_footprints(P.numpy(), coords.numpy(), 96, 96, (4, 8, 8)).sum(1) > 1022).all()
     if what == "feat_inf":
         feat[0, 2, 1, 48, 47] = float("inf")
         feat[1, 0, 3, 47, 48] = -float("inf")

@@ -240,6 +240,28 @@ def test_softargmax_translation_equivariance(device):
     torch.testing.assert_close(b, a + shift, rtol=0, atol=2e-3)
 
 
+@pytest.mark.parametrize("dtype", (torch.float32, torch.bfloat16))
+def test_softargmax_nan_volume_follows_torch(device, dtype):
+    """a joint whose volume holds NaNs — one whole 1,024-voxel pass-1 chunk (its
+    max is NaN) or a single voxel (the chunk's max drops it) — comes out NaN in coordinates
+    and normalised volume, as torch's softmax over the flattened volume (op.py:89) does;
+    the other joints of the frame are untouched."""
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(1, channels=1, volume=16, seed=21)
+    vol = synth.blob_volumes(vb.coords, 3, seed=21).to(dtype)
+    flat = vol.view(1, 3, -1)
+    flat[0, 1, 1024:2048] = float("nan")          # pass-1 chunk 1 of joint 1, all NaN
+    flat[0, 2, 3000] = float("nan")               # one voxel of joint 2
+    sm = torch.softmax(vol.float().view(1, 3, -1), dim=2).view_as(vol)          # op.py:89
+    ref_xyz = torch.einsum("bnxyz,bxyzc->bnc", sm, vb.coords)                  # op.py:94
+    xyz, out = _op().integrate_tensor_3d_with_coordinates(vol.to(device), vb.coords.to(device))
+    xyz, out = xyz.cpu(), out.float().cpu()
+    assert torch.isnan(ref_xyz[0, 1:]).all() and torch.isnan(sm[0, 1:]).all()
+    assert torch.isnan(xyz[0, 1:]).all() and torch.isnan(out[0, 1:]).all()
+    assert torch.isfinite(xyz[0, 0]).all() and torch.isfinite(out[0, 0]).all()
+    assert max_rel(xyz[0, 0].numpy(), ref_xyz[0, 0].numpy()) <= 1e-5
+
+
 # ----------------------------------------------------------------------------- DLT
 @pytest.mark.parametrize("case", ("cfg1", "b3n3", "n8"))
 @pytest.mark.parametrize("use_conf", (True, False))

@@ -369,15 +369,19 @@ def copy_bandwidth(device):
     return _COPY_GBPS
 
 
+def _ratio(a, b):
+    return None if a is None else a / b
+
+
 def roofline(c, r, cfg_name, device=None):
     prec = r.get("precision", "exact")
     traffic, src = measured_traffic(cfg_name, prec)
     out = {"kernel": kernel_name(c, prec), "precision": prec, "bound": "hbm", "achieved": r["achieved_gbps"], "peak": HBM_PEAK_GBPS,
-           "unit": "GB/s", "frac": r["achieved_gbps"] / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": src,
+           "unit": "GB/s", "frac": _ratio(r["achieved_gbps"], HBM_PEAK_GBPS), "traffic": traffic, "traffic_source": src,
            "launch_ms": r["unproject_ms"], "algorithmic_bytes_per_launch": r["launch_bytes"]}
     if device is not None:
         cp = copy_bandwidth(device)
-        out.update(measured_copy_gbps=cp, frac_of_measured_copy=r["achieved_gbps"] / cp)
+        out.update(measured_copy_gbps=cp, frac_of_measured_copy=_ratio(r["achieved_gbps"], cp))
     return out
 
 
@@ -408,10 +412,17 @@ class Workload:
         self.gathered = None
         self.starts = None      # first frame of every rank's shard (set by the caller)
 
-    def reserve_events(self, n):
+    def reserve_events(self, n, stride=4):
         """Pre-create the timing events of n timed steps, so that no Event is constructed
-        inside the timed region (only recorded)."""
+        inside the timed region (only recorded).  Every `stride`-th timed step (the first
+        included) records three events — before and after its unprojection and after its
+        soft-argmax; 0 = no events (no kernel times).  Recording costs GPU time: with events on
+        every step config 2's step took 233.9-234.5 us against 225.7-226.4 us without
+        (profiles/r21_timing_events_ab.txt), so the kernels are timed on a sample of the steps
+        spread over the whole timed region."""
         import torch
+        self.stride, self.nstep = stride, 0
+        n = 0 if stride <= 0 else -(-n // stride)
         self._pool = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(n)]
         # torch creates the HIP event lazily, at its first record(): record each once now, or the
         # timed region pays 3 hipEventCreate per step (~180 us over the driver's 20 steps, r17)
@@ -424,6 +435,10 @@ class Workload:
     def step(self, timed=False, gather=True):
         from mvn_rocm import dist as mdist, op
         J = self.cfg["joints"]
+        if timed:
+            sample = self.stride > 0 and self.nstep % self.stride == 0
+            self.nstep += 1
+            timed = sample
         if timed:
             e0, e1, e2 = self._pool[len(self.ev)]
             e0.record()
@@ -441,9 +456,12 @@ class Workload:
         return xyz, sm
 
     def kernel_ms(self):
+        """(unprojection, soft-argmax) mean ms over the sampled timed steps."""
         import torch
         torch.cuda.synchronize()
         n = len(self.ev)
+        if n == 0:
+            return None, None
         return (sum(a.elapsed_time(b) for a, b, _ in self.ev) / n, sum(b.elapsed_time(c) for _, b, c in self.ev) / n)
 
 
@@ -455,7 +473,7 @@ def run_config(name, args, rank, world, device, clock, cuboid=False, cfg=None, f
     wl = Workload(cfg, rank, world, device, cuboid=cuboid, first_frame=first_frame, global_batch=global_batch,
                   precision=precision)
     wl.starts = starts if starts is not None else [r * cfg["frames"] for r in range(world)]
-    wl.reserve_events(args.steps)
+    wl.reserve_events(args.steps, args.event_stride)
     elapsed = timed_loop(lambda t: wl.step(t), args, clock)
     E = 2 if cfg["dtype"] == torch.bfloat16 else 4
     frames_total = wl.global_batch * args.steps
@@ -467,7 +485,7 @@ def run_config(name, args, rank, world, device, clock, cuboid=False, cfg=None, f
     return dict(cfg=cfg, workload=wl, precision=precision, elapsed=elapsed, fps=frames_total / elapsed,
                 ms_per_step=elapsed / args.steps * 1e3,
                 unproject_ms=unproj_ms, softargmax_ms=sa_ms, launch_bytes=launch_bytes,
-                achieved_gbps=launch_bytes / (unproj_ms * 1e-3) / 1e9,
+                achieved_gbps=(launch_bytes / (unproj_ms * 1e-3) / 1e9) if unproj_ms else None,
                 path_gbps=frame_bytes(cfg, E, cuboid) * frames_total / elapsed / 1e9, telemetry=tel)
 
 
@@ -853,6 +871,9 @@ def main():
                     help="the unprojection arithmetic of the headline and its secondary configs (DESIGN.md §4.1a); "
                          "the other arithmetic is reported beside them")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--event-stride", type=int, default=4,
+                    help="kernel times from HIP events on every K-th timed step (events cost GPU time; "
+                         "1 = every step, 0 = none)")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-in-kernel-coords", action="store_true",
                     help="skip the in-kernel-coordinates run (keeps rocprof kernel means per variant clean)")
@@ -936,7 +957,7 @@ def main():
                                 value=k["fps"], unit="frames/s", ms_per_step=k["ms_per_step"],
                                 unproject_ms=k["unproject_ms"], unproject_algorithmic_bytes_per_launch=k["launch_bytes"],
                                 unproject_achieved_gbps=k["achieved_gbps"],
-                                unproject_frac=k["achieved_gbps"] / HBM_PEAK_GBPS,
+                                unproject_frac=_ratio(k["achieved_gbps"], HBM_PEAK_GBPS),
                                 path_algorithmic_gbps=k["path_gbps"])
     if extras:
         # BASELINE config 4: 8 views, a global batch of 128 frames split over the ranks
@@ -949,7 +970,7 @@ def main():
         cfg4 = dict(workload=c4["label"] + ", global batch 128 split over the ranks", value=128 * args.steps / r4["elapsed"],
                     unit="frames/s", scaling="strong", global_batch=128, frames_per_gpu=count,
                     ms_per_step=r4["ms_per_step"], unproject_ms=r4["unproject_ms"],
-                    unproject_achieved_gbps=r4["achieved_gbps"], unproject_frac=r4["achieved_gbps"] / HBM_PEAK_GBPS,
+                    unproject_achieved_gbps=r4["achieved_gbps"], unproject_frac=_ratio(r4["achieved_gbps"], HBM_PEAK_GBPS),
                     collective=coll, telemetry=r4["telemetry"])
         cfg5 = run_config5(args, rank, world, device, clock)
         if not args.no_in_kernel_coords:

@@ -366,6 +366,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   const __amdgpu_buffer_rsrc_t frs = make_rsrc(fb, uint32_t(size_t(NV) * C * HW * E));
   const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + size_t(b) * C * nvox, uint32_t(size_t(C) * nvox * sizeof(TOut)));
   const uint32_t ooff = act ? uint32_t(vox) * uint32_t(sizeof(TOut)) : kOob;
+
   const uint32_t ooff_cl = act ? uint32_t(vox) * uint32_t(C) * uint32_t(sizeof(TOut)) : kOob;
 
   // LDS byte offsets of each view's north-west and south-west taps (the exact boxes contain

@@ -744,8 +744,8 @@ def parity_check(res):
                            precision=wl.precision)
     bars = ("unproject <= 1e-5 (f32 out) / one bf16 ulp (bf16 out); joints <= 1e-4 (north_star)"
             if wl.precision == "exact" else
-            "fast mode: unproject <= 1e-5 (f32 maps) / one bf16 ulp + 2^-8 max|ref| (bf16 maps); chain joints <= 1e-4 "
-            "(north_star)")
+            "fast mode: unproject <= 1e-4 (f32 maps, north_star's bound) / one bf16 ulp + 2^-8 max|ref| (bf16 maps); "
+            "chain joints <= 1e-4 (north_star)")
     return dict(out, precision=wl.precision, bars=bars, oracle="oracle/mvn_oracle.c via oracle/capi.py",
                 oracle_s=time.perf_counter() - t0)
 

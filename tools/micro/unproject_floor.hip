@@ -13,6 +13,10 @@
 // voxel, the only non-semantic VALU) stored once.  asm volatile("" : "+v") fences make the
 // tap registers opaque per view and group, so nothing is hoisted or shared across groups.
 //
+// Round 6 adds the fast arithmetic (MVN_PRECISION_FAST), modes 4-6: the
+// reciprocal projection, bf16 pixel-pair tap slots (2 per view and 4 channels) sampled by
+// v_dot2_f32_bf16 with bf16 weights, and the max-free view softmax (or sum).
+//
 // Build (CPU container):  tools/micro/build_floor.sh   ->  tools/bin/unproject_floor.so
 // Run   (GPU box):        python tools/micro/unproject_floor.py
 #include <hip/hip_runtime.h>
@@ -25,7 +29,8 @@ using namespace mvn::unproj;
 namespace {
 
 // MODE: 0 projection + taps + softmax, 1 projection + taps + sum, 2 projection only,
-//       3 taps + softmax (weights from the coordinates, no projection)
+//       3 taps + softmax (weights from the coordinates, no projection);
+//       fast arithmetic: 4 projection + dot2 taps + softmax, 5 ... + sum, 6 projection only
 template <int MODE>
 __global__ __launch_bounds__(256) void floor_kernel(const float* __restrict__ P, const float* __restrict__ coords,
                                                     const uint4* __restrict__ seed, float* __restrict__ out,
@@ -38,8 +43,29 @@ __global__ __launch_bounds__(256) void floor_kernel(const float* __restrict__ P,
   const float cx = cp[0], cy = cp[1], cz = cp[2];
 
   f2 wp[NV][2];
+  uint32_t wq[NV][2];
   int fx[NV], fy[NV];
-  if constexpr (MODE != 3) {
+  constexpr bool FASTM = MODE >= 4;
+  if constexpr (FASTM) {
+    const float fW = float(W), fH = float(H);
+    const float ax = fW * __builtin_amdgcn_rcpf(fH), ay = fH * __builtin_amdgcn_rcpf(fW);
+    const float ks = MODE == 4 ? kLog2e : 1.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const Homog hp = homog(Pb + v * 12, cx, cy, cz);
+      const float r = __builtin_amdgcn_rcpf(hp.wh == 0.f ? 1.f : hp.wh);
+      const float ix = __builtin_fmaf(hp.uh, ax * r, -0.5f), iy = __builtin_fmaf(hp.vh, ay * r, -0.5f);
+      const float fx0 = floorf(ix), fy0 = floorf(iy);
+      const bool h = !(hp.wh <= 0.f) & (fx0 >= -1.f) & (fx0 < fW) & (fy0 >= -1.f) & (fy0 < fH);
+      const float tx_ = ix - fx0, sx_ = 1.f - tx_, ty_ = (iy - fy0) * ks, sy_ = ks - ty_;
+      wp[v][0] = f2{h ? sy_ * sx_ : 0.f, h ? sy_ * tx_ : 0.f};
+      wp[v][1] = f2{h ? ty_ * sx_ : 0.f, h ? ty_ * tx_ : 0.f};
+      wq[v][0] = pack_bf16x2(wp[v][0].x, wp[v][0].y);
+      wq[v][1] = pack_bf16x2(wp[v][1].x, wp[v][1].y);
+      fx[v] = h ? int(fx0) : 0;
+      fy[v] = h ? int(fy0) : 0;
+    }
+  } else if constexpr (MODE != 3) {
     bool lane_fast = true;
 #pragma unroll
     for (int v = 0; v < NV; ++v) lane_fast &= div_core_safe(homog(Pb + v * 12, cx, cy, cz));
@@ -68,7 +94,47 @@ __global__ __launch_bounds__(256) void floor_kernel(const float* __restrict__ P,
   }
 
   f2 acc = f2{0.f, 0.f};
-  if constexpr (MODE == 2) {
+  if constexpr (MODE == 6) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      acc += f2{__uint_as_float(wq[v][0]), __uint_as_float(wq[v][1])} + f2{float(fx[v]), float(fy[v])};
+  } else if constexpr (FASTM) {
+    // 2 pixel-pair slots (rows y0, y1) of 4 channels per view, opaque per view and group
+    uint4 s0 = seed[threadIdx.x & 63], s2 = seed[128 + (threadIdx.x & 63)];
+    float dmx = 0.f, dmn = INFINITY;
+#pragma unroll 1
+    for (int c0 = 0; c0 < C; c0 += 4) {
+      f2 sv[2][NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        asm volatile("" : "+v"(s0.x), "+v"(s0.y), "+v"(s0.z), "+v"(s0.w), "+v"(s2.x), "+v"(s2.y), "+v"(s2.z),
+                     "+v"(s2.w));
+        const bf16x2_t w1 = __builtin_bit_cast(bf16x2_t, wq[v][1]);
+        const uint32_t an[4] = {s0.x, s0.y, s0.z, s0.w}, as[4] = {s2.x, s2.y, s2.z, s2.w};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          float o[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            o[h] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, as[2 * q + h]), w1,
+                                                   dot2_bf16_from0(an[2 * q + h], wq[v][0]), false);
+          sv[q][v] = f2{o[0], o[1]};
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if constexpr (MODE == 5) {
+          acc += sv[q][0] + sv[q][1] + sv[q][2] + sv[q][3];
+        } else {
+          f2 den;
+          acc += softmax_pair_log2<NV, false>(sv[q], den);
+          dmx = vmax3f(dmx, den.x, den.y);
+          dmn = vmin3f(dmn, den.x, den.y);
+        }
+      }
+    }
+    acc.x += dmx + dmn;
+  } else if constexpr (MODE == 2) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) acc += wp[v][0] + wp[v][1] + f2{float(fx[v]), float(fy[v])};
   } else {
@@ -116,6 +182,9 @@ extern "C" int floor_run(int mode, const float* P, const float* coords, const vo
     case 1: floor_kernel<1><<<g, blk, 0, s>>>(P, coords, sd, out, nvox, H, W, C); break;
     case 2: floor_kernel<2><<<g, blk, 0, s>>>(P, coords, sd, out, nvox, H, W, C); break;
     case 3: floor_kernel<3><<<g, blk, 0, s>>>(P, coords, sd, out, nvox, H, W, C); break;
+    case 4: floor_kernel<4><<<g, blk, 0, s>>>(P, coords, sd, out, nvox, H, W, C); break;
+    case 5: floor_kernel<5><<<g, blk, 0, s>>>(P, coords, sd, out, nvox, H, W, C); break;
+    case 6: floor_kernel<6><<<g, blk, 0, s>>>(P, coords, sd, out, nvox, H, W, C); break;
     default: return -2;
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;

@@ -13,7 +13,8 @@ import torch  # noqa: E402
 
 from mvn_rocm import _lib, synth  # noqa: E402
 
-MODES = {0: "proj+taps+softmax", 1: "proj+taps+sum", 2: "projection only", 3: "taps+softmax (no proj)"}
+MODES = {0: "proj+taps+softmax", 1: "proj+taps+sum", 2: "projection only", 3: "taps+softmax (no proj)",
+         4: "FAST proj+dot2+softmax", 5: "FAST proj+dot2+sum", 6: "FAST projection only"}
 
 
 def timed(fn, iters=20, rounds=3):
@@ -56,13 +57,15 @@ def main():
         code = 1 if dt == torch.bfloat16 else 0
         vol = torch.empty((B, 32, 64, 64, 64), dtype=dt, device=dev)
         for agg, an in ((2, "softmax"), (0, "sum")):
-            def g(agg=agg):
-                r = lib.mvn_unproject(vb.features.data_ptr(), code, vb.proj.data_ptr(), vb.coords.data_ptr(), None,
-                                      vol.data_ptr(), code, B, 4, 32, 96, 96, 64, 64, 64, agg, 0, stream)
-                assert r == 0, r
-            us = timed(g)
-            print(f"{label:15s} production unproject_x4 {an:8s}    {us:8.1f} us  ({nbytes / us / 8e6:5.3f} of 8 TB/s)",
-                  flush=True)
+            for prec, pn in ((0, "exact"), (1, "FAST")):
+                def g(agg=agg, prec=prec):
+                    r = lib.mvn_unproject_precision(vb.features.data_ptr(), code, vb.proj.data_ptr(),
+                                                    vb.coords.data_ptr(), None, 0, None, vol.data_ptr(), code, 0, B, 4,
+                                                    32, 96, 96, 64, 64, 64, agg, 0, prec, stream)
+                    assert r == 0, r
+                us = timed(g)
+                print(f"{label:15s} production unproject_x4 {pn:5s} {an:8s} {us:8.1f} us  "
+                      f"({nbytes / us / 8e6:5.3f} of 8 TB/s)", flush=True)
 
 
 if __name__ == "__main__":

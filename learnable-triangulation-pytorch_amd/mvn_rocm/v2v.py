@@ -73,14 +73,17 @@ def _inference_only(what, *tensors):
 
 
 def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggregation_method="softmax",
-                            out_dtype=torch.bfloat16, align_corners=False, vol_confidences=None):
+                            out_dtype=torch.bfloat16, align_corners=False, vol_confidences=None, precision=None):
     """unproject_heatmaps (op.py:99-163) written channels-last: (B, Vx, Vy, Vz, C).
     ``coord_volumes`` may be a ``volumetric.Cuboids`` (coordinates formed in-kernel);
     ``vol_confidences`` (B, N, C) is read for 'conf*' aggregation (op.py:147-148), as
-    ``unproject_heatmaps``'s.  Inference-only: no backward (training: ``op.unproject_heatmaps``)."""
+    ``unproject_heatmaps``'s.  Inference-only: no backward (training: ``op.unproject_heatmaps``).
+    ``precision`` as ``op.unproject_heatmaps``'s."""
+    from .op import precision_code
     from .volumetric import Cuboids
     _inference_only("unproject_channels_last", heatmaps, vol_confidences)
     agg = aggregation_code(volume_aggregation_method)
+    prec = precision_code(precision)
     cub = coord_volumes if isinstance(coord_volumes, Cuboids) else None
     feat, proj, conf = unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, volume_aggregation_method, cub)
     if conf is not None:
@@ -90,7 +93,7 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
         # f32 maps into a bf16 volume: the kernels write f32 (no f32 -> bf16 instantiation,
         # mvn_hip.h), rounded to nearest-even by one device cast
         return unproject_channels_last(feat, proj, coord_volumes, volume_aggregation_method, torch.float32,
-                                       align_corners, conf).to(torch.bfloat16)
+                                       align_corners, conf, precision).to(torch.bfloat16)
     fd, od = _dtype_code(feat.dtype), _dtype_code(out_dtype)
     B, N, C, H, W = feat.shape
     if N > 8:
@@ -100,7 +103,7 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
         # written in out_dtype by the kernel itself (bf16 maps into an f32 volume keep f32
         # precision)
         vol = unproject_heatmaps(feat, proj, coord_volumes, volume_aggregation_method, conf,
-                                 align_corners=align_corners, out_dtype=out_dtype)
+                                 align_corners=align_corners, out_dtype=out_dtype, precision=precision)
         return vol.permute(0, 2, 3, 4, 1).contiguous()
     if cub is not None:
         # coordinates formed in-kernel from the per-frame cuboids (bit-identical)
@@ -110,10 +113,10 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
         out = torch.empty((B, V, V, V, C), dtype=out_dtype, device=feat.device)
         if out.numel() == 0:
             return out
-        code = _lib.load().mvn_unproject_cuboid(feat.data_ptr(), fd, proj.data_ptr(), cub.params.data_ptr(),
-                                                int(cub.transfer), cptr, out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC,
-                                                B, N, C, H, W, V, agg, int(align_corners), _stream(feat))
-        _lib.check(code, "mvn_unproject_cuboid")
+        code = _lib.load().mvn_unproject_precision(feat.data_ptr(), fd, proj.data_ptr(), None, cub.params.data_ptr(),
+                                                   int(cub.transfer), cptr, out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC,
+                                                   B, N, C, H, W, V, V, V, agg, int(align_corners), prec, _stream(feat))
+        _lib.check(code, "mvn_unproject_precision")
         return out
     coords = coord_volumes.float().contiguous()
     if coords.dim() != 5 or coords.shape[0] != B or coords.shape[4] != 3:
@@ -123,10 +126,10 @@ def unproject_channels_last(heatmaps, proj_matricies, coord_volumes, volume_aggr
     out = torch.empty((B, Vx, Vy, Vz, C), dtype=out_dtype, device=feat.device)
     if out.numel() == 0:                  # empty batch: the empty volume, as unproject_heatmaps
         return out
-    code = _lib.load().mvn_unproject_ex(feat.data_ptr(), fd, proj.data_ptr(), coords.data_ptr(), cptr,
-                                        out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC, B, N, C, H, W, Vx, Vy, Vz, agg,
-                                        int(align_corners), _stream(feat))
-    _lib.check(code, "mvn_unproject_ex")
+    code = _lib.load().mvn_unproject_precision(feat.data_ptr(), fd, proj.data_ptr(), coords.data_ptr(), None, 0, cptr,
+                                               out.data_ptr(), od, _lib.MVN_LAYOUT_NDHWC, B, N, C, H, W, Vx, Vy, Vz,
+                                               agg, int(align_corners), prec, _stream(feat))
+    _lib.check(code, "mvn_unproject_precision")
     return out
 
 
@@ -151,28 +154,32 @@ class Basic3DBlockFront(nn.Module):
 
 def unproject_v2v_front(heatmaps, proj_matricies, coord_volumes, packed, scale, shift,
                         volume_aggregation_method="softmax", out_dtype=torch.float32, group_frames=0,
-                        align_corners=False, vol_confidences=None):
+                        align_corners=False, vol_confidences=None, precision=None):
     """Config 5 in one call (``mvn_unproject_v2v_front``): unproject_heatmaps (op.py:99-163)
     written channels-last bf16, then the front block relu(bn(conv3d_7)), pipelined over frame
     groups through a workspace of one group's intermediate (default: 8 frames at V = 64,
     within half of the MALL).  ``coord_volumes`` may be a ``volumetric.Cuboids``.  Equal to
     ``v2v_front(unproject_channels_last(...))`` bit for bit.  'conf*' aggregation reads
     ``vol_confidences`` (B, N, C), as the volumetric model does (triangulation.py:349).
-    Inference-only: no backward (the eval-mode BatchNorm fold is inference by construction)."""
+    Inference-only: no backward (the eval-mode BatchNorm fold is inference by construction).
+    ``precision='fast'`` runs the two steps (the one-call C pipeline is the
+    exact arithmetic)."""
+    from .op import precision_code
     from .volumetric import Cuboids
     _inference_only("unproject_v2v_front", heatmaps, vol_confidences)
     agg = aggregation_code(volume_aggregation_method)
+    fast = precision_code(precision) == _lib.MVN_PRECISION_FAST
     cub = coord_volumes if isinstance(coord_volumes, Cuboids) else None
     feat, proj, conf = unproject_inputs(heatmaps, proj_matricies, vol_confidences, agg, volume_aggregation_method, cub)
     fd, od = _dtype_code(feat.dtype), _dtype_code(out_dtype)
     B, N, C, H, W = feat.shape
     if C != CIN:
         raise RuntimeError(f"unproject_v2v_front needs {CIN} heatmap channels, got {C}")
-    if N > 8 or B == 0:
+    if N > 8 or B == 0 or fast:
         # more than 8 views (the channels-last kernels take N <= 8) or an empty batch: the two
         # steps, which handle both
         cl = unproject_channels_last(feat, proj, coord_volumes, volume_aggregation_method, align_corners=align_corners,
-                                     vol_confidences=conf)
+                                     vol_confidences=conf, precision=precision)
         return v2v_front(cl, packed, scale, shift, out_dtype)
     if cub is not None:
         coords, V = None, cub.volume_size

@@ -241,3 +241,43 @@ def test_fast_in_kernel_coordinates(device):
     ref = capi.unproject(bf16_bits(vb.features), vb.proj.cpu().numpy(), co, "softmax", feat_bf16_bits=True)
     out = _unproject(vb.features, vb.proj, cub, "softmax")
     assert_bf16_fast(out, ref)
+
+
+def test_fast_volumetric_chain_matches_reference_model(golden, device):
+    """VolumetricTriangulationNet.forward as recorded from the reference (tests/golden/chains.npz:
+    4 views x 32 ch x 32^2 -> 32^3, softmax, V2V stand-in = channels [0:17]) with the fast
+    unprojection: volume <= 1e-4 (f32 bar), joints <= 1e-4 (north_star), both coordinate forms."""
+    from mvn_rocm import op, volumetric
+    d = golden("chains.npz")
+    side, V = float(d["vol_side"]), d["vol_coords"].shape[1]
+    cv = volumetric.build_coord_volumes(d["vol_base"], side, V, d["vol_thetas"], "mpii", False, device=device)
+    cub = volumetric.build_cuboids(d["vol_base"], side, V, d["vol_thetas"], "mpii", False, device=device)
+    f, P = _t(d["vol_features"], device), _t(d["vol_proj"], device)
+    sub = (slice(None), slice(None), slice(None, None, 4), slice(None, None, 4), slice(None, None, 4))
+    for coords in (cv, cub):
+        vol = _unproject(f, P, coords, "softmax")
+        assert max_rel(vol.cpu().numpy()[sub], d["vol_unprojected_sub"]) <= F32_TOL
+        xyz, _ = op.integrate_tensor_3d_with_coordinates(vol[:, :17], coords, True)
+        assert max_rel(xyz.cpu().numpy(), d["vol_kp3d"]) <= 1e-4
+
+
+def test_fast_cfg5_channels_last_full_size(device):
+    """BASELINE config 5's unprojection (bf16, channels-last, 64^3) in the fast arithmetic: the
+    transpose of the fast NCDHW volume bit for bit, within the fast bar of the C oracle; the
+    one-call pipeline in fast mode equals the two steps."""
+    from mvn_rocm import synth, v2v
+    vb = synth.volumetric_batch(1, dtype=torch.bfloat16, device=device, seed=57)
+    cl = v2v.unproject_channels_last(vb.features, vb.proj, vb.coords, "softmax", precision="fast")
+    nc = _unproject(vb.features, vb.proj, vb.coords, "softmax")
+    assert torch.equal(cl.view(torch.int16), nc.permute(0, 2, 3, 4, 1).contiguous().view(torch.int16))
+    ref = capi.unproject(bf16_bits(vb.features), vb.proj.cpu().numpy(), vb.coords.cpu().numpy(), "softmax",
+                         feat_bf16_bits=True)
+    assert_bf16_fast(nc, ref)
+    g = torch.Generator().manual_seed(57)
+    w = torch.randn((16, 32, 7, 7, 7), generator=g) * 0.02
+    packed, scale, shift = v2v.fold_basic3d_block(w, torch.randn(16, generator=g) * 0.1, torch.rand(16, generator=g) + 0.5,
+                                                  torch.randn(16, generator=g) * 0.1, torch.zeros(16), torch.ones(16),
+                                                  device=device)
+    y1 = v2v.unproject_v2v_front(vb.features, vb.proj, vb.coords, packed, scale, shift, "softmax", precision="fast")
+    y2 = v2v.v2v_front(cl, packed, scale, shift, torch.float32)
+    assert torch.equal(y1, y2)

@@ -49,5 +49,8 @@ for cfg in 3 4; do
   bash tools/pmc_mem.sh "$out/mem_cfg${cfg}_fast" 'unproject_x4' python3 tools/prof_unproject.py $cfg 5 fast
 done
 echo "memory-pipe passes done"
+timeout -k 10 120 python3 tools/repack_cost.py > "$out/repack_cost.txt" 2>&1
+python3 tools/step_gaps.py "$out/kt_cfg2/kt_kernel_trace.csv" > "$out/step_gaps_cfg2.txt" 2>&1 || true
+python3 tools/step_gaps.py "$out/kt_cfg3/kt_kernel_trace.csv" > "$out/step_gaps_cfg3.txt" 2>&1 || true
 bash tools/pmc_cycles.sh "$out/v2v_cycles" learnable-triangulation-pytorch_amd/mvn_rocm/libmvn_hip.so > "$out/v2v_cycles.txt" 2>&1
 echo "v2v cycle pass done"

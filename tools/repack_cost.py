@@ -29,7 +29,7 @@ def main():
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / 50 * 1e3
         nb = 2 * f.numel() * f.element_size()
-        print(f"{label}: repack {us:.1f} us ({nb / us / 1e6:.0f} GB/s of read + write)", flush=True)
+        print(f"{label}: repack {us:.1f} us ({nb / us / 1e3:.0f} GB/s of read + write)", flush=True)
 
 
 if __name__ == "__main__":

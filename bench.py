@@ -414,15 +414,17 @@ class Workload:
 
     def reserve_events(self, n, stride=4):
         """Pre-create the timing events of n timed steps, so that no Event is constructed
-        inside the timed region (only recorded).  Every `stride`-th timed step (the first
-        included) records three events — before and after its unprojection and after its
+        inside the timed region (only recorded).  Every `stride`-th timed step (steps stride-1,
+        2 stride-1, ...) records three events — before and after its unprojection and after its
         soft-argmax; 0 = no events (no kernel times).  Recording costs GPU time: with events on
         every step config 2's step took 233.9-234.5 us against 225.7-226.4 us without
         (profiles/r21_timing_events_ab.txt), so the kernels are timed on a sample of the steps
         spread over the whole timed region."""
         import torch
+        if 0 < n < stride:          # short timed regions: at least the last step
+            stride = n
         self.stride, self.nstep = stride, 0
-        n = 0 if stride <= 0 else -(-n // stride)
+        n = 0 if stride <= 0 else n // stride
         self._pool = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(n)]
         # torch creates the HIP event lazily, at its first record(): record each once now, or the
         # timed region pays 3 hipEventCreate per step (~180 us over the driver's 20 steps, r17)
@@ -436,7 +438,8 @@ class Workload:
         from mvn_rocm import dist as mdist, op
         J = self.cfg["joints"]
         if timed:
-            sample = self.stride > 0 and self.nstep % self.stride == 0
+            # the last step of every stride (the first timed step follows the fence's idle GPU)
+            sample = self.stride > 0 and self.nstep % self.stride == self.stride - 1
             self.nstep += 1
             timed = sample
         if timed:

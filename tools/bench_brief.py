@@ -7,7 +7,7 @@ def main():
     d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
     r = d.get("roofline") or {}
     print(f"headline {d['value']:.0f} {d['unit']} ({d.get('precision')}), {d['ms_per_step'] * 1e3:.1f} us/step; "
-          f"unproject {r.get('launch_ms', 0) * 1e3:.1f} us frac {r.get('frac')}, softargmax {d.get('softargmax_ms')}")
+          f"unproject {(r.get('launch_ms') or 0) * 1e3:.1f} us frac {r.get('frac')}, softargmax {d.get('softargmax_ms')}")
     print("  parity", d.get("parity"))
     s = d.get("secondary") or {}
     if s:

@@ -58,6 +58,17 @@ template <> struct X4Shape<3> {
   static constexpr int NV = 8, G = 2, TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 2048, MC = 3, WAVES = 3;
   static constexpr int STORE_F32 = 0;
 };
+// 4 views, bf16 maps, fast arithmetic (pixel-pair slots): an 8x8x8 tile of 512 threads —
+// 1.92 instead of 2.65 staged pixels per voxel (tools/footprints.py: the footprint of a
+// cube grows slower than its volume), one chunk slot per thread (the largest footprint at
+// the bench geometry is 421 chunks), two 2,048-slot buffers (2 blocks per CU, 4 waves/SIMD)
+template <> struct X4Shape<4> {
+  static constexpr int NV = 4, G = 4, TX = 8, TY = 8, TZ = 8, THREADS = 512, SLOTS = 1536, MC = 1, WAVES = 6;
+  static constexpr int STORE_F32 = kStorePolicyF32;
+};
+#ifndef MVN_FAST_BF16_SHAPE
+#define MVN_FAST_BF16_SHAPE 4
+#endif
 
 // LDS slot: one pixel's G channels as f32
 template <int G> struct SlotT;
@@ -508,9 +519,20 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     if constexpr (SMXF && kDeferredGuard) {
       if (__builtin_amdgcn_ballot_w64(!(dmx <= 0x1p120f) || !(dmn >= 0x1p-100f))) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the fast values' stores land first
+        // the voxel's coordinates formed again from its index (opaque to the compiler, so that
+        // the prologue's coordinates are not kept live across the channel loop for this path)
+        int v2 = vox;
+        asm volatile("" : "+v"(v2));
+        float c2[3];
+        if (cub) {
+          cuboid_coord(cub + b * MVN_CUBOID_FLOATS, Vx, v2 / (Vy * Vz), (v2 / Vz) % Vy, v2 % Vz, transfer, c2);
+        } else {
+          const float* cp = coords + (size_t(b) * nvox + v2) * 3;
+          c2[0] = cp[0]; c2[1] = cp[1]; c2[2] = cp[2];
+        }
         if (act)
-          gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + (out_cl ? size_t(vox) * C : vox),
-                                       out_cl ? 1 : nvox, NV, C, H, W, cx, cy, cz, align_corners);
+          gather_voxel<AGG, TIn, TOut>(fb, Pb, cfb, out + size_t(b) * C * nvox + (out_cl ? size_t(v2) * C : v2),
+                                       out_cl ? 1 : nvox, NV, C, H, W, c2[0], c2[1], c2[2], align_corners);
       }
     }
   };
@@ -619,6 +641,9 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  // fast: the tap offsets before the staging starts, so that the per-view base pixels die here
+  // (live into the multi-pass branch they spilled at 6 waves per SIMD)
+  if constexpr (FAST != 0) tap_slots();
   if (npass == 1) {
     // ---- one pass: up to MC chunks per thread (chunk t + kThreads * i over the views'
     // concatenated chunk ranges), two LDS buffers, the next group's loads in flight --------
@@ -647,7 +672,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
         if (wfirst + kWaves * kLanesW * i < total) write_group(buf, pre[i], s0[i], mask[i]);
     };
     issue(0);
-    tap_slots();
+    if constexpr (FAST == 0) tap_slots();
     commit(stageA);
     __syncthreads();
     // A group's outputs are stored after the NEXT group's commit: on gfx950 vmcnt counts
@@ -676,7 +701,7 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   }
 
   // ---- several passes of whole views per channel group (close cameras) ---------------
-  tap_slots();
+  if constexpr (FAST == 0) tap_slots();
   for (int c0 = 0; c0 < C; c0 += G) {
     f2 sv[NP][NV];
     for (int pass = 0; pass < npass; ++pass) {
@@ -729,6 +754,18 @@ int launch_x4(const void* feat, const float* P, const float* coords, const float
     const long long nb = (long long)B * ((Vx + S::TX - 1) / S::TX) * ((Vy + S::TY - 1) / S::TY) *
                          ((Vz + S::TZ - 1) / S::TZ);
     if (nb > INT_MAX) return MVN_ERR_SHAPE;
+    if constexpr (K == 2 && CL == 0 && MVN_FAST_BF16_SHAPE == 4) {
+      if (fast) {       // bf16 maps, NCDHW, fast arithmetic: the 8x8x8 tile (X4Shape<4>)
+        using S4 = X4Shape<4>;
+        const long long nb4 = (long long)B * ((Vx + S4::TX - 1) / S4::TX) * ((Vy + S4::TY - 1) / S4::TY) *
+                              ((Vz + S4::TZ - 1) / S4::TZ);
+        if (nb4 > INT_MAX) return MVN_ERR_SHAPE;
+        unproject_x4<AGG, TIn, TOut, 4, 0, 1><<<int(nb4), S4::THREADS, 0, s>>>(
+            static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, C, H, W, Vx,
+            Vy, Vz, align_corners, budget);
+        return launch_ok() ? MVN_OK : MVN_ERR_LAUNCH;
+      }
+    }
     if (fast)
       unproject_x4<AGG, TIn, TOut, K, CL, 1><<<int(nb), S::THREADS, 0, s>>>(
           static_cast<const TIn*>(feat), P, coords, cub, transfer, conf, static_cast<TOut*>(out), B, C, H, W, Vx, Vy,

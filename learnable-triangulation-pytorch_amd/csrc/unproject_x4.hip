@@ -61,7 +61,10 @@ template <> struct X4Shape<3> {
 // 4 views, bf16 maps, fast arithmetic (pixel-pair slots): an 8x8x8 tile of 512 threads —
 // 1.92 instead of 2.65 staged pixels per voxel (tools/footprints.py: the footprint of a
 // cube grows slower than its volume), one chunk slot per thread (the largest footprint at
-// the bench geometry is 421 chunks), two 2,048-slot buffers (2 blocks per CU, 4 waves/SIMD)
+// the bench geometry is 421 chunks), two 1,536-slot buffers: 49 KB of LDS and 78 VGPRs, so 3
+// blocks per CU, 6 waves per SIMD (cfg3 503 -> 437 us against 4 waves, r21).  The f32 and
+// exact kernels need 113-117 VGPRs on this tile and spill in the tap loop (2.4-3.2x slower,
+// profiles/r21_ab_tile_occupancy_negatives.txt)
 template <> struct X4Shape<4> {
   static constexpr int NV = 4, G = 4, TX = 8, TY = 8, TZ = 8, THREADS = 512, SLOTS = 1536, MC = 1, WAVES = 6;
   static constexpr int STORE_F32 = kStorePolicyF32;
@@ -139,6 +142,8 @@ __global__ __launch_bounds__(X4Shape<K>::THREADS) __attribute__((amdgpu_waves_pe
   constexpr int TX = S::TX, TY = S::TY, TZ = S::TZ;
   constexpr int kThreads = S::THREADS, kBuf = S::SLOTS, MC = S::MC, kWaves = kThreads / kWave;
   static_assert(TX * TY * TZ == kThreads, "one voxel per thread");
+  // validated tiles: TX 4 or 8, TY 8, TZ 8 or 16 (an 8x4x16 variant was not bit-identical, r21)
+  static_assert(TY == 8 && (TX == 4 || TX == 8), "tile shape outside the validated set");
   // PAIR: bf16 pixel-pair slots — dword k of the slot at pixel (x, y) holds channel k's
   // (x, x+1) bf16 pair, so a voxel-view reads 2 slots (rows y0, y1) per 4 channels instead of
   // 4, and each row is one v_dot2_f32_bf16 against the (west, east) bf16 weight pair.  A

@@ -530,12 +530,14 @@ def run_config5(args, rank, world, device, clock, cuboid=False):
 
     elapsed = timed_loop(step, args, clock)
     conv_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
-    tel = telemetry(device, step)
     tflops = V2V_FLOP_PER_FRAME * B / (conv_ms * 1e-3) / 1e12
     # the same work through the one-call pipeline (mvn_unproject_v2v_front: frame groups of 8
     # through a 134 MB workspace instead of the 1.07 GB whole-batch intermediate)
     one = timed_loop(lambda t: v2v.unproject_v2v_front(vb.features, vb.proj, coords, packed, scale, shift, "softmax",
                                                        torch.bfloat16), args, clock)
+    # telemetry after BOTH timed loops: its burst of extra GPU work (this config runs at the
+    # package power limit) would otherwise heat the chip between them
+    tel = telemetry(device, step)
     pin = None if cuboid else dict(feat=vb.features, proj=vb.proj, coords=vb.coords, last=tuple(last),
                                    w_bf16=w.bfloat16().float(), scale=scale, shift=shift)
     return dict(parity_inputs=pin, workload=cfg["label"], value=B * world * args.steps / elapsed, unit="frames/s",

@@ -693,9 +693,10 @@ def _np_feat(t):
 
 
 def _within_fast_bar(got, ref):
-    """The fast mode's bar for a bf16 volume: one bf16 ulp of the f32
-    oracle + 2^-8 x max|ref| (bf16 bilinear weights)."""
-    return _within_one_bf16_ulp(got, ref, 2.0 ** -8)
+    """The fast mode's bar for a bf16 volume of the bench's softmax step:
+    one bf16 ulp of the f32 oracle + 2^-7 x max|ref| (bf16 bilinear weights, which the view
+    softmax puts in the exponent; tests/test_gpu_fast.py's softmax bar)."""
+    return _within_one_bf16_ulp(got, ref, 2.0 ** -7)
 
 
 def parity_unproject(feat, proj, coords, vol, J, frames, xyz=None, layout="ncdhw", precision="exact"):
@@ -749,7 +750,7 @@ def parity_check(res):
                            precision=wl.precision)
     bars = ("unproject <= 1e-5 (f32 out) / one bf16 ulp (bf16 out); joints <= 1e-4 (north_star)"
             if wl.precision == "exact" else
-            "fast mode: unproject <= 1e-4 (f32 maps, north_star's bound) / one bf16 ulp + 2^-8 max|ref| (bf16 maps); "
+            "fast mode: unproject <= 1e-4 (f32 maps, north_star's bound) / one bf16 ulp + 2^-7 max|ref| (bf16 maps, softmax); "
             "chain joints <= 1e-4 (north_star)")
     return dict(out, precision=wl.precision, bars=bars, oracle="oracle/mvn_oracle.c via oracle/capi.py",
                 oracle_s=time.perf_counter() - t0)

@@ -155,8 +155,8 @@ int mvn_unproject_ex(const void* feat, int feat_dtype,
  * (op.py:99-163).  Exactly one of coords (B, Vx, Vy, Vz, 3) and cuboids (B, 18; then
  * Vx = Vy = Vz, N <= 8) is non-NULL.  precision = MVN_PRECISION_EXACT is bit-identical
  * to those entry points; MVN_PRECISION_FAST computes the same function within the
- * north_star tolerance (f32 maps: <= 1e-5 max-rel of the volume; bf16 maps: one bf16 ulp
- * + 2^-8 max|ref|; validity masks unchanged), measured in DESIGN.md §4.1a.
+ * north_star tolerance (f32 maps: <= 1e-4 max-rel of the volume, measured 2-4e-5; bf16 maps: one bf16 ulp
+ * + 2^-8 max|ref|, 2^-7 for softmax; validity masks unchanged), measured in DESIGN.md §4.1a.
  */
 int mvn_unproject_precision(const void* feat, int feat_dtype,
                             const float* proj, const float* coords, const float* cuboids, int transfer_cmu,

@@ -8,8 +8,12 @@ Bars (written here):
   f32 maps            volume max-rel <= 1e-4 (north_star's fp32 bound; measured 2-4e-5: one ulp of
                       a reciprocal-based pixel coordinate moves a bilinear sample by ~1e-5 px x the
                       neighbouring pixels' difference)
-  bf16 maps, f32 out  volume max-rel <= 2^-8
-  bf16 maps, bf16 out every value within one bf16 ulp of the f32 oracle + 2^-8 max|ref|
+  bf16 maps, f32 out  volume max-rel <= 2^-8; softmax 2^-7 (the bf16 weights enter the exponent: a
+                      sample's error 2^-9 * M (M = the largest tap magnitude) moves each view's
+                      softmax weight by up to the same relative amount, times the spread of the
+                      samples over the views; measured 3.1-3.9e-3 over seeds and shapes,
+                      tools/fast_bf16_error_probe.py, profiles/r21_fast_bf16_error_probe.txt)
+  bf16 maps, bf16 out every value within one bf16 ulp of the f32 oracle + the f32-out bar x max|ref|
   joints              soft-argmax of the fast volume vs of the oracle volume <= 1e-4 (north_star)
   validity            voxels behind every camera (op.py:121) are exactly 0, as in the reference
 """
@@ -25,6 +29,12 @@ pytestmark = pytest.mark.gpu
 METHODS = ("sum", "max", "softmax", "conf")
 F32_TOL = 1e-4
 BF16_REL = 2.0 ** -8
+BF16_SOFTMAX_REL = 2.0 ** -7
+
+
+def bf16_bar(method):
+    """The bf16-maps bar of one aggregation (module docstring)."""
+    return BF16_SOFTMAX_REL if method == "softmax" else BF16_REL
 
 
 def _t(a, device, dtype=None):
@@ -41,9 +51,9 @@ def bf16_ulp(ref):
     return np.where(ref == 0, 0.0, np.ldexp(1.0, e - 8))
 
 
-def assert_bf16_fast(out16, ref):
+def assert_bf16_fast(out16, ref, method):
     got = out16.float().cpu().numpy().astype(np.float64)
-    bound = bf16_ulp(ref) + BF16_REL * np.abs(ref).max()
+    bound = bf16_ulp(ref) + bf16_bar(method) * np.abs(ref).max()
     err = np.abs(got - ref)
     assert (err <= bound).all(), float((err / np.maximum(bound, 1e-45)).max())
 
@@ -99,9 +109,9 @@ def test_fast_cfg3_bf16_full_size(device, method):
                          feat_bf16_bits=True)
     out16 = _unproject(vb.features, vb.proj, vb.coords, method, _t(conf, device))
     assert out16.dtype == torch.bfloat16
-    assert_bf16_fast(out16, ref)
+    assert_bf16_fast(out16, ref, method)
     out32 = _unproject(vb.features, vb.proj, vb.coords, method, _t(conf, device), out_dtype=torch.float32)
-    assert max_rel(out32.cpu().numpy(), ref) <= BF16_REL
+    assert max_rel(out32.cpu().numpy(), ref) <= bf16_bar(method)
     assert 0.2 < (ref != 0).mean()
 
 
@@ -152,7 +162,23 @@ def test_fast_every_staging_path(device, dtype, path, method):
     with _lib.unproject_knobs(budget):
         out = _unproject(vb.features.to(device), vb.proj.to(device), vb.coords.to(device), method,
                          out_dtype=torch.float32)
-    assert max_rel(out.cpu().numpy(), ref) <= (F32_TOL if dtype == torch.float32 else BF16_REL)
+    assert max_rel(out.cpu().numpy(), ref) <= (F32_TOL if dtype == torch.float32 else bf16_bar(method))
+
+
+@pytest.mark.parametrize("dtype", (torch.float32, torch.bfloat16))
+@pytest.mark.parametrize("method", ("sum", "softmax"))
+def test_fast_ragged_non_cubic_volume(device, dtype, method):
+    """A (13, 21, 10) coordinate volume: every axis leaves a partial tile of the fast kernels'
+    8x8x8 (bf16) and 4x8x16 (f32) tiles; inactive voxels neither write nor stage."""
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(2, channels=8, heatmap=64, volume=24, seed=41, dtype=dtype)
+    coords = vb.coords[:, :13, :21, :10].contiguous()
+    feat = bf16_bits(vb.features) if dtype == torch.bfloat16 else vb.features.numpy()
+    ref = capi.unproject(feat, vb.proj.numpy(), coords.numpy(), method, feat_bf16_bits=dtype == torch.bfloat16)
+    out = _unproject(vb.features.to(device), vb.proj.to(device), coords.to(device), method, out_dtype=torch.float32)
+    assert out.shape == (2, 8, 13, 21, 10)
+    assert max_rel(out.cpu().numpy(), ref) <= (F32_TOL if dtype == torch.float32 else bf16_bar(method))
+    assert 0.2 < (ref != 0).mean()
 
 
 # ----------------------------------------------------------------------------- range guard, NaN, validity
@@ -169,7 +195,7 @@ def test_fast_softmax_range_guard(device, dtype, scale):
     out = _unproject(feat.to(device), vb.proj.to(device), vb.coords.to(device), "softmax", out_dtype=torch.float32)
     got = out.cpu().numpy()
     assert np.isfinite(got).all()
-    assert max_rel(got, ref) <= (F32_TOL if dtype == torch.float32 else BF16_REL)
+    assert max_rel(got, ref) <= (F32_TOL if dtype == torch.float32 else bf16_bar("softmax"))
 
 
 @pytest.mark.parametrize("dtype", (torch.float32, torch.bfloat16))
@@ -191,7 +217,7 @@ def test_fast_nan_features_propagate(device, dtype):
     assert nr.sum() > 50
     assert (nr != ng).sum() <= max(4, nr.sum() // 50)
     fin = ~(nr | ng)
-    assert max_rel(got[fin], ref[fin]) <= (F32_TOL if dtype == torch.float32 else BF16_REL)
+    assert max_rel(got[fin], ref[fin]) <= (F32_TOL if dtype == torch.float32 else bf16_bar("softmax"))
 
 
 @pytest.mark.parametrize("dtype", (torch.float32, torch.bfloat16))
@@ -241,7 +267,7 @@ def test_fast_in_kernel_coordinates(device):
     co = restate_np.coord_volumes(base, 2500.0, 64, theta, "coco", False)
     ref = capi.unproject(bf16_bits(vb.features), vb.proj.cpu().numpy(), co, "softmax", feat_bf16_bits=True)
     out = _unproject(vb.features, vb.proj, cub, "softmax")
-    assert_bf16_fast(out, ref)
+    assert_bf16_fast(out, ref, "softmax")
 
 
 def test_fast_volumetric_chain_matches_reference_model(golden, device):
@@ -273,7 +299,7 @@ def test_fast_cfg5_channels_last_full_size(device):
     assert torch.equal(cl.view(torch.int16), nc.permute(0, 2, 3, 4, 1).contiguous().view(torch.int16))
     ref = capi.unproject(bf16_bits(vb.features), vb.proj.cpu().numpy(), vb.coords.cpu().numpy(), "softmax",
                          feat_bf16_bits=True)
-    assert_bf16_fast(nc, ref)
+    assert_bf16_fast(nc, ref, "softmax")
     g = torch.Generator().manual_seed(57)
     w = torch.randn((16, 32, 7, 7, 7), generator=g) * 0.02
     packed, scale, shift = v2v.fold_basic3d_block(w, torch.randn(16, generator=g) * 0.1, torch.rand(16, generator=g) + 0.5,

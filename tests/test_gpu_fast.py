@@ -97,6 +97,31 @@ def test_fast_cfg4_eight_views(device, method):
     assert max_rel(out.cpu().numpy(), ref) <= F32_TOL
 
 
+@pytest.mark.parametrize("method", ("sum", "softmax"))
+def test_fast_eight_views_bf16(device, method):
+    """8 views of bf16 maps (2-channel f32 slots: the fast projection and softmax, no pixel
+    pairs) against the oracle on the same bf16 bits, at the bf16 bar."""
+    from mvn_rocm import synth
+    vb = synth.volumetric_batch(1, n_views=8, channels=8, volume=32, seed=46, dtype=torch.bfloat16)
+    ref = capi.unproject(bf16_bits(vb.features), vb.proj.numpy(), vb.coords.numpy(), method, feat_bf16_bits=True)
+    out = _unproject(vb.features.to(device), vb.proj.to(device), vb.coords.to(device), method,
+                     out_dtype=torch.float32)
+    assert max_rel(out.cpu().numpy(), ref) <= bf16_bar(method)
+    assert 0.2 < (ref != 0).mean()
+
+
+@pytest.mark.parametrize("n_views", (1, 3, 5))
+def test_fast_falls_back_to_exact_where_it_does_not_apply(device, n_views):
+    """View counts other than 4 and 8 run the exact kernels in either mode:
+    precision='fast' returns the exact volume bit for bit."""
+    from mvn_rocm import op, synth
+    vb = synth.volumetric_batch(1, n_views=n_views, channels=8, volume=16, seed=47)
+    f, P, c = vb.features.to(device), vb.proj.to(device), vb.coords.to(device)
+    fast = op.unproject_heatmaps(f, P, c, "softmax", precision="fast")
+    exact = op.unproject_heatmaps(f, P, c, "softmax", precision="exact")
+    assert torch.equal(fast.view(torch.int32), exact.view(torch.int32))
+
+
 # ----------------------------------------------------------------------------- bf16 maps (pixel pairs, v_dot2)
 @pytest.mark.parametrize("method", METHODS)
 def test_fast_cfg3_bf16_full_size(device, method):

@@ -44,8 +44,12 @@ template <> struct X4Shape<0> {   // 4 views, f32 maps
   static constexpr int NV = 4, G = 4, TX = 4, TY = 8, TZ = 16, THREADS = 512, SLOTS = 2048, MC = 2, WAVES = 4;
   static constexpr int STORE_F32 = kStorePolicyF32;
 };
-template <> struct X4Shape<2> {   // 4 views, bf16 maps (widened exactly to f32 slots when staged)
-  static constexpr int NV = 4, G = 4, TX = 4, TY = 8, TZ = 8, THREADS = 256, SLOTS = 1024, MC = 2, WAVES = 4;
+// 4 views, bf16 maps (widened exactly to f32 slots when staged): an 8x8x8 tile of 512 threads,
+// 1.7 instead of 2.2 staged pixels per voxel at 4 waves per SIMD (2 blocks of 66 KB per CU; its
+// 115 VGPRs keep 6 waves out of reach): cfg3 softmax 535 -> 512 us against the 4x8x8 tile of 256
+// threads (r21, profiles/r21_ab_exact_bf16_tile.txt)
+template <> struct X4Shape<2> {
+  static constexpr int NV = 4, G = 4, TX = 8, TY = 8, TZ = 8, THREADS = 512, SLOTS = 2048, MC = 1, WAVES = 4;
   static constexpr int STORE_F32 = kStorePolicyF32;
 };
 // 8 views (BASELINE config 4, CMU-style): the footprint of 8 views doubles, so slots of 2

@@ -67,14 +67,16 @@ def _tile_areas(proj, coords, H, W, tile=(4, 8, 16)):
     return tile_footprints(proj, coords, H, W, tile)
 
 
-@pytest.mark.parametrize("n_views", (4, 8))
+@pytest.mark.parametrize("n_views,dt", ((4, "f32"), (4, "bf16"), (8, "f32")))
 @pytest.mark.parametrize("path", ("multipass", "fallback"))
 @pytest.mark.parametrize("method", ("sum", "softmax"))
-def test_x4_staging_paths(device, path, method, n_views):
+def test_x4_staging_paths(device, path, method, n_views, dt):
     """LDS budgets that force several staging passes of whole views, and single views
-    larger than the budget (global-gather fallback) — against the oracle."""
+    larger than the budget (global-gather fallback) — against the oracle (bf16 maps: on
+    the same bf16 bits, f32 out)."""
     vb, conf = _batch(device, 71, heatmap=64, volume=32, channels=8, n_views=n_views)
-    tile = (4, 8, 16) if n_views == 4 else (4, 8, 8)
+    # X4Shape tiles: 4 views f32 4x8x16, 4 views bf16 8x8x8, 8 views 4x8x8
+    tile = (4, 8, 8) if n_views == 8 else (8, 8, 8) if dt == "bf16" else (4, 8, 16)
     areas = _tile_areas(vb.proj.numpy(), vb.coords.numpy(), 64, 64, tile)
     if path == "multipass":
         budget = int(areas.max()) + 64
@@ -82,8 +84,11 @@ def test_x4_staging_paths(device, path, method, n_views):
     else:
         budget = int(np.median(areas[areas > 0]))
         assert (areas.max(1) > budget - 1).any() and (areas.max(1) <= budget - 1).any()
-    out = _run(vb.features.to(device), vb.proj.to(device), vb.coords.to(device), method, None, lds_slots=budget)
-    ref = capi.unproject(vb.features.numpy(), vb.proj.numpy(), vb.coords.numpy(), method)
+    feat = vb.features.to(torch.bfloat16) if dt == "bf16" else vb.features
+    out = _run(feat.to(device), vb.proj.to(device), vb.coords.to(device), method, None, out_dtype=torch.float32,
+               lds_slots=budget)
+    bits = feat.view(torch.int16).numpy().view(np.uint16) if dt == "bf16" else feat.numpy()
+    ref = capi.unproject(bits, vb.proj.numpy(), vb.coords.numpy(), method, feat_bf16_bits=dt == "bf16")
     if method == "softmax":
         assert max_rel(out.cpu().numpy(), ref) <= 1e-5
     else:

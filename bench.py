@@ -328,7 +328,7 @@ def kernel_name(c, precision="exact"):
     p = "" if precision == "exact" else (", fast: bf16 pixel-pair slots, v_dot2" if t == "bf16" and c["views"] == 4
                                         else ", fast")
     if c["views"] == 4:      # the chunk-staged kernel (csrc/unproject_x4.hip), tile per dtype
-        return f"unproject_x4<softmax, {t}, {t}, tile {'4x8x16' if t == 'float' else '4x8x8'}{p}>"
+        return f"unproject_x4<softmax, {t}, {t}, tile {'4x8x16' if t == 'float' else '8x8x8'}{p}>"
     return f"unproject_x4<softmax, {t}, {t}, 8 views, 2-channel slots, tile 4x8x8{p}>"
 
 
